@@ -1,0 +1,328 @@
+#!/usr/bin/env python
+"""bench.py -- throughput of CohereEnhancedVectorDB's three-phase search on MI355X.
+
+Metric (BASELINE.json): queries/sec + recall@10 vs float32, d=1024 3-phase
+search at 1/2/4/8 GPUs.  Default workload = BASELINE config 2: 3-phase search
+over a 1M x 1024 synthetic corpus (SURVEY.md section 8(d) generator), query
+batches of nq = 1024, k = 10, binary_oversample = 10, int8_oversample = 3.
+
+One step = one three-phase search of the whole nq-query batch:
+  K1 vrq_search3_scan (Phase I Hamming scan, per-chunk exact top-K)
+  K2 vrq_search3_finish (exact merge + Phase II + Phase III + stable sorts)
+  [N > 1: one RCCL all_gather of the per-shard candidates + vrq_merge_shards]
+Inputs are HBM-resident before the timed region.  With --gpus N the 1M-row
+corpus is row-sharded over N ranks (strong scaling: the same corpus and the
+same query batch per step for every N); results are identical for every N.
+
+--config c3 runs the Phase-I-only HBM-roofline case instead (uniform random
+codes, queries = corpus rows with 64-256 flipped bits).
+
+rank 0 prints ONE JSON line (see README of the driver contract).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from vectorragquantization_amd import _native as N  # noqa: E402
+from vectorragquantization_amd import synth  # noqa: E402
+from vectorragquantization_amd.dist import gather_candidates, merge_shards, pack_candidates, unpack_candidates  # noqa: E402
+
+METRIC = "queries/sec + recall@10 vs float32, d=1024 3-phase search at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0                          # MI355X spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--n", type=int, default=None, help="corpus rows (total over all ranks)")
+    ap.add_argument("--nq", type=int, default=None, help="queries per step")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--binary-oversample", type=int, default=10)
+    ap.add_argument("--int8-oversample", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=512, help="queries timed on the host CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--recall-sample", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-recall", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Pipeline:
+    """One rank's search step with event-bracketed kernels on torch's current stream."""
+
+    def __init__(self, codes, x8, norms, row0, n_total, qf, qb, k, osb, osi, world, phase1_only=False):
+        self.lib = N.load()
+        self.codes, self.x8, self.norms, self.row0 = codes, x8, norms, row0
+        self.qf, self.qb = qf, qb
+        self.k, self.K, self.K3 = k, min(k * osb, n_total), k * osi
+        self.world = world
+        self.phase1 = phase1_only
+        self.flags = N.VRQ_SEARCH_PHASE1_ONLY if phase1_only else (N.VRQ_SEARCH_SHARD if world > 1 else 0)
+        nq = qf.shape[0]
+        dev = codes.device
+        self.m = codes.shape[0]
+        ws = self.lib.vrq_search3_workspace_size(self.m, 1024, nq, self.K)
+        self.ws = torch.empty((max(ws, 8),), dtype=torch.uint8, device=dev)
+        self.list_bytes = ws
+        kout = self.K if self.flags & (N.VRQ_SEARCH_SHARD | N.VRQ_SEARCH_PHASE1_ONLY) else k
+        self.cnt = torch.empty((nq,), dtype=torch.int32, device=dev)
+        self.rows = torch.empty((nq, kout), dtype=torch.int64, device=dev)
+        self.dist = torch.empty((nq, kout), dtype=torch.int32, device=dev)
+        self.s2 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
+        self.s3 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
+        self.ids = None
+        self.ev = []
+        self.final = None
+
+    def step(self, record: bool):
+        L, st = self.lib, N.stream_handle(self.codes.device)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        N.check(L.vrq_search3_scan(N.ptr(self.codes), self.m, 1024, N.ptr(self.qb), self.qb.shape[0], self.K,
+                                   N.ptr(self.ws), self.ws.numel(), st), "scan")
+        if record:
+            e[1].record()
+        N.check(L.vrq_search3_finish(N.ptr(self.codes), N.ptr(self.x8), N.ptr(self.norms), None, self.m, 1024,
+                                     self.row0, N.ptr(self.qf), self.qf.shape[0], self.k, self.K, self.K3,
+                                     self.flags, N.ptr(self.cnt), N.ptr(self.rows), N.ptr(self.dist),
+                                     N.ptr(self.s2), N.ptr(self.s3), N.ptr(self.ws), self.ws.numel(), st),
+                "finish")
+        if record:
+            e[2].record()
+        if self.world > 1 and not self.phase1:
+            nq = self.qf.shape[0]
+            ids = self.rows  # external id = global row for the synthetic corpus
+            buf = gather_candidates(pack_candidates(self.cnt, self.rows, ids, self.dist, self.s2, self.s3))
+            gc, gr, gi, gd, g2, g3 = unpack_candidates(buf, self.world, nq, self.K)
+            self.final = merge_shards(gc, gr, gd, g2, g3, self.k, self.K3)
+        else:
+            self.final = (self.cnt, self.rows, self.dist, self.s2, self.s3)
+        if record:
+            e[3].record()
+            self.ev.append(e)
+
+    def kernel_ms(self):
+        sc = [a.elapsed_time(b) for a, b, _, _ in self.ev]
+        fi = [b.elapsed_time(c) for _, b, c, _ in self.ev]
+        co = [c.elapsed_time(d) for _, _, c, d in self.ev]
+        return float(np.mean(sc)), float(np.mean(fi)), float(np.mean(co))
+
+
+def recall_at_10(top_rows, qf, n_total, rank, world, dev, sample):
+    """recall@10 of the 3-phase top-10 vs exact float32 inner product (CohereVectorDBFloat semantics)."""
+    qs = qf[:sample]
+    C = synth.centres(1024, dev)
+    cs = synth.chunk_grid(n_total)
+    r0, r1 = synth.shard_range(n_total, rank, world)
+    best_v = torch.full((qs.shape[0], 10), -float("inf"), device=dev)
+    best_i = torch.full((qs.shape[0], 10), -1, dtype=torch.int64, device=dev)
+    for c in range(r0 // cs, (r1 + cs - 1) // cs):
+        a, b = c * cs, min((c + 1) * cs, n_total)
+        F = synth.float_rows(a, b - a, 1024, dev, C, chunk=c)
+        S = qs @ F.T
+        v, i = torch.topk(torch.cat([best_v, S], 1), 10, dim=1)
+        cand = torch.cat([best_i, torch.arange(a, b, device=dev).expand(qs.shape[0], -1)], 1)
+        best_v, best_i = v, torch.gather(cand, 1, i)
+        del F, S
+    if world > 1:
+        gv = [torch.empty_like(best_v) for _ in range(world)]
+        gi = [torch.empty_like(best_i) for _ in range(world)]
+        dist.all_gather(gv, best_v)
+        dist.all_gather(gi, best_i)
+        v, i = torch.topk(torch.cat(gv, 1), 10, dim=1)
+        best_i = torch.gather(torch.cat(gi, 1), 1, i)
+    gt = best_i.cpu().numpy()
+    got = top_rows[:sample].cpu().numpy()
+    return float(np.mean([len(set(a[a >= 0]) & set(b)) / 10.0 for a, b in zip(got, gt)]))
+
+
+def cpu_baseline(codes_h, x8_h, qf_h, qb_h, k, osb, osi, threads, sample, gpu_rows=None):
+    """Restated reference path on the host: FAISS hammings_knn_hc in C (OpenMP over queries)
+    + the reference's NumPy Phase II / III per query.  Returns (dict, parity_ok)."""
+    import ctypes as C
+    import subprocess
+    from oracle import oracle_np as O
+    so = os.path.join(HERE, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(so):
+        subprocess.check_call([os.path.join(HERE, "oracle", "build.sh")])
+    lib = C.CDLL(so)
+    lib.oracle_hamming_knn.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_void_p, C.c_int]
+    nq = min(sample, qf_h.shape[0])
+    K = min(k * osb, codes_h.shape[0])
+    qb = np.ascontiguousarray(qb_h[:nq])
+    D = np.empty((nq, K), np.int32)
+    I = np.empty((nq, K), np.int64)
+    t0 = time.perf_counter()
+    lib.oracle_hamming_knn(codes_h.ctypes.data, codes_h.shape[0], 128, qb.ctypes.data, nq, K, D.ctypes.data,
+                           I.ctypes.data, threads)
+    t1 = time.perf_counter()
+    out_rows = []
+    for q in range(nq):
+        rows = I[q][I[q] >= 0]
+        pm = 2 * np.unpackbits(codes_h[rows], axis=1).astype(np.int32) - 1
+        s2 = pm.astype(np.float64) @ qf_h[q].astype(np.float64)
+        o2 = sorted(range(rows.shape[0]), key=lambda j: -s2[j])[: k * osi]
+        r3 = rows[o2]
+        s3 = []
+        for r in r3:
+            v = x8_h[r]
+            nrm = np.linalg.norm(v)
+            s3.append(-np.inf if nrm == 0 else float(qf_h[q].dot(v)) / nrm)
+        o3 = sorted(range(len(s3)), key=lambda j: -s3[j])[:k]
+        out_rows.append(r3[o3])
+    t2 = time.perf_counter()
+    parity = None
+    if gpu_rows is not None:
+        g = gpu_rows[:nq]
+        parity = float(np.mean([len(set(a) & set(b[b >= 0])) / max(1, len(a)) for a, b in zip(out_rows, g)]))
+    qps = nq / (t2 - t0)
+    return {"value": qps, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{nq} queries of the same batch over the full {codes_h.shape[0]}-row corpus; Phase I = C "
+                      f"restatement of FAISS hammings_knn_hc (OpenMP over queries, {threads} threads, "
+                      f"{t1 - t0:.2f} s), Phases II/III = the reference NumPy per-query code (1 thread, "
+                      f"{t2 - t1:.2f} s). FAISS itself is not available offline.",
+            "phase1_s": t1 - t0, "phase23_s": t2 - t1}, parity
+
+
+def pmc_traffic(tag):
+    """Per-launch HBM bytes of the scan kernel from a committed rocprofv3 --pmc summary
+    (FETCH_SIZE KB x2 for gfx950 16-B streams + WRITE_SIZE KB), or None."""
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*{tag}*pmc*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return float(d["scan_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    phase1 = a.config == "c3"
+    n = a.n or (100_000_000 if phase1 else 1_000_000)
+    nq = a.nq or (8 if phase1 else 1024)
+    N.load()
+    t_setup = time.perf_counter()
+    if phase1:
+        r0, r1 = synth.shard_range(n, rank, world)
+        codes = synth.random_codes(r1 - r0, device=dev, seed=synth.SEED + 77 * rank)
+        x8 = torch.empty((1, 1024), dtype=torch.int8, device=dev)
+        norms = torch.empty((1,), dtype=torch.float64, device=dev)
+        qb, _ = synth.flip_queries(codes, nq)
+        if world > 1:
+            dist.broadcast(qb, 0)
+        qf = torch.zeros((nq, 1024), dtype=torch.float32, device=dev)
+        row0 = r0
+    else:
+        shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+        codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
+        qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
+
+    P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, phase1)
+    for _ in range(a.warmup):
+        P.step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        P.step(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    T = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([T], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        T = float(tt.item())
+    scan_ms, fin_ms, coll_ms = P.kernel_ms()
+
+    top_rows = P.final[1]
+    rec = None
+    if not a.no_recall and not phase1:
+        rec = recall_at_10(top_rows, qf, n, rank, world, dev, min(a.recall_sample, nq))
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    m = codes.shape[0]
+    K = P.K
+    alg_bytes = m * 128 + nq * 128 + nq * K * 12
+    achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
+    tag = f"{a.config}_n{n}_nq{nq}_g{world}"
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(tag), "kernel": "hamming_scan_kernel (K1)",
+            "kernel_ms": scan_ms, "algorithmic_bytes_per_launch": alg_bytes}
+    valu_ops = nq * m * 64  # 32 v_xor + 32 v_bcnt lane-ops per (query, 1024-bit row)
+    roof_valu = {"bound": "valu", "achieved": valu_ops / (scan_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS,
+                 "unit": "T lane-ops/s", "frac": valu_ops / (scan_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS}
+    out = {
+        "metric": METRIC, "value": nq * a.steps / T, "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8" if phase1 else "u8+f64",
+        "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)"
+                if not phase1 else "synthetic (uniform random 1024-bit codes, bit-flipped-row queries)",
+        "config": {"workload": ("BASELINE config 3: Phase-I-only Hamming top-k" if phase1 else
+                                "BASELINE config 2: CohereEnhancedVectorDB 3-phase search") +
+                               f", {n} x 1024 corpus, nq={nq} queries per step",
+                   "corpus_rows": n, "nq": nq, "k": a.k, "binary_oversample": a.binary_oversample,
+                   "int8_oversample": a.int8_oversample, "parallelism": f"row-shard x{world} + RCCL all_gather"
+                   if world > 1 else "1 GPU"},
+        "recall_at_10": rec,
+        "phase_ms": {"scan_K1": scan_ms, "finish_K2": fin_ms, "allgather_merge": coll_ms},
+        "roofline": roof, "roofline_valu": roof_valu,
+    }
+    if world == 1 and not a.no_cpu_baseline and not phase1:
+        cb, parity = cpu_baseline(codes.cpu().numpy(), x8.cpu().numpy(), qf.cpu().numpy(), qb.cpu().numpy(),
+                                  a.k, a.binary_oversample, a.int8_oversample, a.cpu_threads, a.cpu_sample,
+                                  top_rows.cpu().numpy())
+        out["cpu_baseline"] = cb
+        out["cpu_gpu_top10_agreement"] = parity
+    elif world == 1 and not a.no_cpu_baseline and phase1:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+/*
+ * vrq.h -- C ABI of libvrq.so, the MI355X (gfx950) hot path of
+ * aitrailblazer/VectorRAGQuantization re-built as hand-written HIP kernels.
+ *
+ * The reference reaches its compute through two un-vendored native
+ * dependencies (FAISS C++ for Phase I, NumPy for Phases II/III and the
+ * encoders).  Each entry point below replaces one of those call sites; the
+ * reference location is cited per function (paths relative to the reference
+ * checkout).  The Python host layer (vectorragquantization_amd) binds these
+ * symbols with ctypes; the cgo / JNI / ctypes stubs a maintainer would add on
+ * the reference side are in INTEGRATION.md.
+ *
+ * Conventions (all functions):
+ *   - every pointer is a DEVICE pointer owned by the caller (allocated e.g. by
+ *     torch); the library never allocates, frees or synchronises;
+ *   - all work is enqueued on `stream` (a hipStream_t passed as void*, NULL =
+ *     the null stream) and is stream-ordered; no host threads, no global
+ *     mutable state, so concurrent calls on different streams are safe;
+ *   - return VRQ_OK (0) or a negative VRQ_E* code; never abort, never throw;
+ *     vrq_strerror() maps a code to text.
+ *   - row indices are int64; "rows" are internal (insertion-order) indices of
+ *     the caller's shard, reported as row_offset + local row (global row).
+ */
+#ifndef VRQ_H_
+#define VRQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VRQ_ABI_VERSION 1
+
+#define VRQ_OK 0
+#define VRQ_EINVAL (-1)       /* bad argument (null pointer, negative size, ...) */
+#define VRQ_EHIP (-2)         /* a HIP runtime call or kernel launch failed */
+#define VRQ_EUNSUPPORTED (-3) /* shape outside what the kernels implement */
+#define VRQ_EWORKSPACE (-4)   /* workspace smaller than *_workspace_size() */
+
+/* flags for vrq_search3 */
+#define VRQ_SEARCH_PHASE1_ONLY 1 /* stop after Phase I (FAISS IndexBinaryFlat::search) */
+#define VRQ_SEARCH_SHARD 2       /* sharded mode: return all K Phase-I candidates in
+                                    (dist,row) order with Phase-II AND Phase-III
+                                    scores, no Phase II/III sort (merged later by
+                                    vrq_merge_shards) */
+
+/* encoder modes for vrq_encode */
+#define VRQ_ENC_INT8_GLOBAL 0  /* VectorDBInt8Global._quantize_to_int8 + _to_binary */
+#define VRQ_ENC_INT16_GLOBAL 1 /* VectorDBInt16Global._quantize_to_int16 + _to_binary */
+#define VRQ_ENC_INT4_GLOBAL 2  /* VectorDBInt4Global._quantize_to_int4 (limit ignored) + _to_binary */
+#define VRQ_ENC_INT8_LOCAL 3   /* VectorDBInt8._quantize_to_int8 (+min/max) + _to_binary */
+#define VRQ_ENC_INT4_LOCAL 4   /* VectorDBInt4._quantize_to_int4 (+min/max) + _to_binary */
+#define VRQ_ENC_BIN_INT16 5    /* VectorDBInt16._to_binary on int16 input */
+#define VRQ_ENC_COHERE 6       /* synthetic Cohere provider: int8 (global limit) + ubinary = packbits(x > 0) */
+
+int vrq_abi_version(void);
+const char* vrq_strerror(int code);
+
+/* ---------------------------------------------------------------------------
+ * Phase I -- exhaustive Hamming k-NN over packed codes.
+ * Replaces faiss.IndexBinaryFlat::search (hammings_knn_hc) reached from
+ *   CohereEnhancedVectorDB.py:267-268 (and VectorDBInt8Global.py:224-225,
+ *   VectorDBInt16.py, VectorDBInt4*.py, VectorDBInt16Global.py search()).
+ * codes      u8[n, code_bytes]    (code_bytes = d/8; 128 for d = 1024)
+ * queries    u8[nq, code_bytes]
+ * out_dist   i32[nq, k]  ascending (dist, row) -- FAISS order; missing = INT32_MAX
+ * out_rows   i64[nq, k]  row_offset + row; missing = -1
+ * Supported: code_bytes in {64, 128, 256}, 1 <= k <= 1024, n < 2^40.
+ * ------------------------------------------------------------------------- */
+size_t vrq_hamming_topk_workspace_size(int64_t n, int32_t code_bytes, int32_t nq, int32_t k);
+int vrq_hamming_topk(const uint8_t* codes, int64_t n, int32_t code_bytes, int64_t row_offset,
+                     const uint8_t* queries, int32_t nq, int32_t k, int32_t* out_dist,
+                     int64_t* out_rows, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused three-phase search -- replaces CohereEnhancedVectorDB.search
+ *   (CohereEnhancedVectorDB.py:247-322) for a batch of nq queries:
+ *   Phase I   top-K by Hamming (K = binary_k = min(k*binary_oversample, ntotal), :267-275)
+ *   Phase II  s2 = q . (2*unpackbits(code)-1) in float64 (:283-293); stable sort desc (:296)
+ *   Phase III s3 = float(q . int8 [f32]) / ||int8||_2 [f64], -inf if 0 (:302-318);
+ *             over the first K3 = k*int8_oversample (:297); stable sort desc; first k (:321-322)
+ * x8     int8[n, dim]   (the RocksDict "int8" value, :221)
+ * norms  f64[n]         ||x8 row||_2 (vrq_int8_row_norms), as np.linalg.norm (:308)
+ * rescore_row  i64[n] or NULL: row whose code/int8 Phases II/III use for Phase-I row r.
+ *        IndexBinaryIDMap2::reconstruct(id) returns the row of the LAST add of an id
+ *        (rev_map, :286) and the doc store keeps the last value (:221,303); when an id
+ *        occurs on several rows pass rev_map[id_map[r]], else NULL (identity).
+ * qf     f32[nq, dim], qb u8[nq, dim/8]
+ * outputs [nq, kout] where kout = k (or K with VRQ_SEARCH_SHARD):
+ *   out_count i32[nq]; out_rows i64; out_dist i32; out_binary f64; out_cosine f64
+ * dim must be 1024 (code_bytes 128) in this ABI version.
+ * ------------------------------------------------------------------------- */
+size_t vrq_search3_workspace_size(int64_t n, int32_t dim, int32_t nq, int32_t K);
+int vrq_search3(const uint8_t* codes, const int8_t* x8, const double* norms, const int64_t* rescore_row,
+                int64_t n, int32_t dim, int64_t row_offset, const float* qf, const uint8_t* qb, int32_t nq, int32_t k,
+                int32_t K, int32_t K3, int32_t flags, int32_t* out_count, int64_t* out_rows,
+                int32_t* out_dist, double* out_binary, double* out_cosine, void* workspace,
+                size_t workspace_bytes, void* stream);
+
+/* The two launches vrq_search3 is made of, for callers that time or overlap them:
+ * vrq_search3_scan   -- K1, the Phase-I scan: per-chunk exact top-K lists into `workspace`
+ * vrq_search3_finish -- K2, exact merge of those lists + Phases II/III + the sorts
+ * (same arguments as vrq_search3; the workspace carries the lists between them). */
+int vrq_search3_scan(const uint8_t* codes, int64_t n, int32_t dim, const uint8_t* qb, int32_t nq,
+                     int32_t K, void* workspace, size_t workspace_bytes, void* stream);
+int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* norms,
+                       const int64_t* rescore_row, int64_t n, int32_t dim, int64_t row_offset,
+                       const float* qf, int32_t nq, int32_t k, int32_t K, int32_t K3, int32_t flags,
+                       int32_t* out_count, int64_t* out_rows, int32_t* out_dist, double* out_binary,
+                       double* out_cosine, const void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Merge of per-shard candidate tuples after the RCCL all-gather (multi-GPU
+ * row sharding; the reference is single-process, so this reproduces the
+ * single-index semantics of CohereEnhancedVectorDB.py:267-322 exactly):
+ *   global top-K by (dist, global row) -> stable sort by s2 desc -> first K3
+ *   -> stable sort by s3 desc -> first k.
+ * Inputs are the VRQ_SEARCH_SHARD outputs of S shards stacked [S, nq, K]
+ * (counts i32[S, nq]); shard s must own a contiguous global row range below
+ * shard s+1's.  out_src (nullable) i32[nq, k] receives s*K + p, the position of
+ * each result in the stacked inputs (to fetch per-candidate payloads such as
+ * external ids).
+ * ------------------------------------------------------------------------- */
+int vrq_merge_shards(int32_t nshards, int32_t nq, int32_t K, const int32_t* counts,
+                     const int64_t* rows, const int32_t* dist, const double* s2,
+                     const double* s3, int32_t k, int32_t K3, int32_t* out_count,
+                     int64_t* out_rows, int32_t* out_dist, double* out_binary,
+                     double* out_cosine, int32_t* out_src, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Stand-alone Phase II / Phase III candidate rescoring (the per-candidate
+ * loops of CohereEnhancedVectorDB.py:283-293 and :302-318).
+ * cand_rows i64[nq, ncand] local rows (negative = skip, output NaN).
+ * ------------------------------------------------------------------------- */
+int vrq_rescore_binary(const float* qf, int32_t nq, int32_t dim, const uint8_t* codes, int64_t n,
+                       const int64_t* cand_rows, int32_t ncand, double* out, void* stream);
+int vrq_rescore_int8_cosine(const float* qf, int32_t nq, int32_t dim, const int8_t* x8,
+                            const double* norms, int64_t n, const int64_t* cand_rows,
+                            int32_t ncand, double* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Encoders -- the VectorDBInt{4,8,16}{,Global} quantize + _to_binary path:
+ *   VectorDBInt8Global.py:130-142,154-160   VectorDBInt16Global.py:130-142,154-160
+ *   VectorDBInt4Global.py:129-164,190-196   VectorDBInt8.py:114-126,140-146
+ *   VectorDBInt4.py:116-154,186-192          VectorDBInt16.py:148-157
+ * x       f32[n, dim] (i16[n, dim] for VRQ_ENC_BIN_INT16)
+ * codes   u8[n, dim/8]           packbits(x > mean(x)) MSB-first (or x > 0 for COHERE)
+ * q       i8[n, dim] | i16[n, dim] | i8[n, (dim+1)/2] (int4 nibbles) | unused
+ * minmax  f64[n, 2] (local modes only; may be NULL otherwise)
+ * limit   global clip limit (Global modes / COHERE), as passed by the caller
+ * dim must be a multiple of 8 and <= 8192.
+ * ------------------------------------------------------------------------- */
+int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit, uint8_t* codes,
+               void* q, double* minmax, void* stream);
+
+/* np.linalg.norm(int8 row) in float64 (CohereEnhancedVectorDB.py:308), computed once at add time */
+int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VRQ_H_ */

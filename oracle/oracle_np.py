@@ -1,0 +1,337 @@
+"""NumPy restatement of the reference hot path -- TEST INFRASTRUCTURE ONLY.
+
+See ``oracle/__init__.py`` for the usage rule (checker / CPU baseline only).
+Every function cites the reference ``file:line`` it restates; paths are
+relative to the reference checkout (aitrailblazer/VectorRAGQuantization @
+2025-02-18).  FAISS is not vendored in the reference; its semantics are
+restated from ``IndexBinaryFlat::search`` -> ``hammings_knn_hc`` (heap top-k,
+insert iff ``dis < heap_top``, heap ordered by (dist, id), final reorder).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+INT32_MAX = np.iinfo(np.int32).max
+
+# byte -> popcount table (Phase I restatement)
+_POPCNT8 = np.array([bin(i).count("1") for i in range(256)], dtype=np.int32)
+
+
+# --------------------------------------------------------------------------
+# Phase I: FAISS IndexBinaryFlat / IndexBinaryIDMap2 restatement
+# --------------------------------------------------------------------------
+def hamming_distances(codes: np.ndarray, queries: np.ndarray, chunk: int = 8192) -> np.ndarray:
+    """All-pairs Hamming distance, i32[nq, n].
+
+    Restates ``hc.hamming(bs2_)`` of FAISS ``hammings_knn_hc`` reached from
+    ``CohereEnhancedVectorDB.py:268``: popcount(q XOR code) over the packed
+    ``ubinary`` bytes (bit order is irrelevant for Hamming).
+    """
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    queries = np.ascontiguousarray(queries, dtype=np.uint8)
+    nq, n = queries.shape[0], codes.shape[0]
+    out = np.empty((nq, n), dtype=np.int32)
+    for s in range(0, n, chunk):
+        c = codes[s:s + chunk]
+        x = queries[:, None, :] ^ c[None, :, :]
+        out[:, s:s + chunk] = _POPCNT8[x].sum(axis=2, dtype=np.int32)
+    return out
+
+
+def binary_flat_search(codes: np.ndarray, queries: np.ndarray, k: int):
+    """FAISS ``IndexBinaryFlat::search`` restatement -> (D i32[nq,k], I i64[nq,k]).
+
+    ``hammings_knn_hc`` keeps a max-heap ordered by (dist, id), inserts a row
+    only if ``dis < heap_top`` (strict) while rows arrive in increasing
+    internal index, and ``heap_reorder`` emits ascending (dist, id).  The result
+    is therefore the k smallest rows under the lexicographic (dist asc,
+    internal index asc) order; missing slots (n < k) are (INT32_MAX, -1).
+    Call site: ``CohereEnhancedVectorDB.py:267-268``.
+    """
+    nq = queries.shape[0]
+    n = codes.shape[0]
+    D = np.full((nq, k), INT32_MAX, dtype=np.int32)
+    I = np.full((nq, k), -1, dtype=np.int64)
+    if n == 0 or k == 0:
+        return D, I
+    dist = hamming_distances(codes, queries)
+    kk = min(k, n)
+    idx = np.arange(n, dtype=np.int64)
+    for q in range(nq):
+        order = np.lexsort((idx, dist[q]))[:kk]
+        D[q, :kk] = dist[q][order]
+        I[q, :kk] = order
+    return D, I
+
+
+class IndexBinaryIDMap2:
+    """NumPy restatement of ``faiss.IndexBinaryIDMap2(faiss.IndexBinaryFlat(d))``.
+
+    Only the protocol the reference exercises: ``add_with_ids``
+    (``CohereEnhancedVectorDB.py:217``), ``search`` (``:268``),
+    ``reconstruct`` (``:286``), ``remove_ids`` (``:334``), ``ntotal``
+    (``:247,267,350``).  ``remove_ids`` compacts storage preserving the order
+    of survivors; ``rev_map`` maps an external id to its (last added) row.
+    """
+
+    def __init__(self, d: int = 1024):
+        self.d = d
+        self.code_size = d // 8
+        self.xb = np.zeros((0, self.code_size), dtype=np.uint8)
+        self.id_map = np.zeros((0,), dtype=np.int64)
+        self.rev_map: dict[int, int] = {}
+
+    @property
+    def ntotal(self) -> int:
+        return int(self.xb.shape[0])
+
+    def add_with_ids(self, x: np.ndarray, ids: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=np.uint8).reshape(-1, self.code_size)
+        ids = np.asarray(ids, dtype=np.int64).reshape(-1)
+        base = self.ntotal
+        self.xb = np.concatenate([self.xb, x], axis=0)
+        self.id_map = np.concatenate([self.id_map, ids])
+        for j, e in enumerate(ids.tolist()):
+            self.rev_map[e] = base + j
+
+    def search(self, q: np.ndarray, k: int):
+        D, I = binary_flat_search(self.xb, np.asarray(q, dtype=np.uint8).reshape(-1, self.code_size), k)
+        L = np.where(I >= 0, self.id_map[np.maximum(I, 0)] if self.ntotal else -1, -1)
+        return D, L.astype(np.int64)
+
+    def reconstruct(self, key) -> np.ndarray:
+        return self.xb[self.rev_map[int(key)]].copy()
+
+    def remove_ids(self, ids) -> int:
+        rm = set(int(i) for i in np.asarray(ids).reshape(-1).tolist())
+        keep = np.array([int(e) not in rm for e in self.id_map.tolist()], dtype=bool)
+        nrm = int((~keep).sum())
+        self.xb = self.xb[keep]
+        self.id_map = self.id_map[keep]
+        self.rev_map = {int(e): j for j, e in enumerate(self.id_map.tolist())}
+        return nrm
+
+
+# --------------------------------------------------------------------------
+# Phases II / III: literal restatement of CohereEnhancedVectorDB.search
+# --------------------------------------------------------------------------
+def three_phase_search(index: IndexBinaryIDMap2, doc_int8: dict, doc_text: dict,
+                       query_float: np.ndarray, query_ubinary: np.ndarray,
+                       k: int = 10, binary_oversample: int = 10,
+                       int8_oversample: int = 3) -> list:
+    """Per-query restatement of ``CohereEnhancedVectorDB.search`` (``:227-322``).
+
+    ``doc_int8`` maps external id -> int8[d] (the RocksDict ``"int8"`` value,
+    ``:221,303-307``), ``doc_text`` maps id -> text.  Arithmetic follows the
+    reference exactly: Phase II ``float32 . int32 -> float64`` dot over
+    ``2*unpackbits-1`` (``:286-290``), Phase III ``float(float32 . int8)`` /
+    ``np.linalg.norm(int8)`` (float64) with ``-inf`` for a zero norm
+    (``:307-313``), Python's stable sorts (``:274,296,321``).
+    """
+    if index.ntotal == 0:                                          # :247-249
+        return []
+    qf = np.asarray(query_float, dtype=np.float32).reshape(1, -1)  # :260
+    qb = np.asarray(query_ubinary, dtype=np.uint8).reshape(1, -1)  # :261
+    binary_k = min(k * binary_oversample, index.ntotal)            # :267
+    distances, ids = index.search(qb, binary_k)                    # :268
+    hits = [{"doc_id": int(i), "score_hamming": int(d)}
+            for i, d in zip(ids[0], distances[0]) if i != -1]      # :269-273
+    hits.sort(key=lambda h: h["score_hamming"])                    # :274
+    cands = hits[:k * binary_oversample]                           # :275
+    if not cands:
+        return []
+    for h in cands:                                                # :283-293
+        bits = np.unpackbits(index.reconstruct(h["doc_id"]), axis=-1).astype(np.int32)
+        h["score_binary"] = float(qf[0].dot(2 * bits - 1))
+    cands.sort(key=lambda h: h["score_binary"], reverse=True)      # :296
+    resc = cands[:k * int8_oversample]                             # :297
+    final = []
+    for h in resc:                                                 # :302-318
+        v = doc_int8.get(h["doc_id"])
+        if v is None:
+            continue
+        v = np.asarray(v, dtype=np.int8)
+        nrm = np.linalg.norm(v)
+        h["score_cosine"] = -np.inf if nrm == 0 else float(qf[0].dot(v)) / nrm
+        h["doc"] = doc_text.get(h["doc_id"], "N/A")
+        final.append(h)
+    final.sort(key=lambda h: h["score_cosine"], reverse=True)      # :321
+    return final[:k]                                               # :322
+
+
+def three_phase_batch(codes: np.ndarray, int8: np.ndarray, ids: np.ndarray,
+                      qf: np.ndarray, qb: np.ndarray, k: int = 10,
+                      binary_oversample: int = 10, int8_oversample: int = 3):
+    """Array form of ``three_phase_search`` for many queries (oracle for the GPU path).
+
+    Rows are internal indices (insertion order); ``ids`` is the id map.
+    Returns per query a dict of arrays: ``row`` (internal index), ``doc_id``,
+    ``hamming``, ``binary``, ``cosine`` for the final top-k, plus the
+    intermediate ``p1_rows``/``p1_dist`` (Phase I), ``p2_rows``/``p2_score``
+    (Phase II, in stable-sorted order).  Phase II uses a float64 GEMV (exact:
+    every partial sum of float32 values of an embedding fits in 53 bits, so
+    the result equals the reference's per-candidate ``ddot``); Phase III uses
+    float32 ``sdot`` per candidate exactly like ``:312``.
+    """
+    n = codes.shape[0]
+    out = []
+    if n == 0:
+        return [None] * qf.shape[0]
+    binary_k = min(k * binary_oversample, n)
+    D, I = binary_flat_search(codes, qb, binary_k)
+    norms = int8_row_norms(int8)
+    for q in range(qf.shape[0]):
+        rows = I[q][I[q] >= 0]
+        dist = D[q][: rows.shape[0]]
+        pm = 2 * np.unpackbits(codes[rows], axis=1).astype(np.int32) - 1
+        s2 = pm.astype(np.float64) @ qf[q].astype(np.float64)
+        o2 = sorted(range(rows.shape[0]), key=lambda j: -s2[j])   # stable, desc
+        o2 = np.array(o2[: k * int8_oversample], dtype=np.int64)
+        r3 = rows[o2]
+        s3 = np.empty(r3.shape[0], dtype=np.float64)
+        for j, r in enumerate(r3.tolist()):
+            nrm = norms[r]
+            s3[j] = -np.inf if nrm == 0 else float(qf[q].dot(int8[r])) / nrm
+        o3 = np.array(sorted(range(r3.shape[0]), key=lambda j: -s3[j])[:k], dtype=np.int64)
+        fin = o2[o3]
+        out.append({
+            "p1_rows": rows, "p1_dist": dist,
+            "p2_score_by_p1": s2,
+            "p2_order": o2,
+            "row": rows[fin], "doc_id": ids[rows[fin]], "hamming": dist[fin],
+            "binary": s2[fin], "cosine": s3[o3],
+        })
+    return out
+
+
+def int8_row_norms(x: np.ndarray) -> np.ndarray:
+    """``np.linalg.norm(doc_int8)`` per row (float64), ``CohereEnhancedVectorDB.py:308``."""
+    x = np.asarray(x)
+    return np.sqrt((x.astype(np.float64) ** 2).sum(axis=1)) if x.ndim == 2 else np.linalg.norm(x)
+
+
+def float_ip_topk(F: np.ndarray, Q: np.ndarray, k: int) -> np.ndarray:
+    """Exact float32 inner-product top-k ids (``CohereVectorDBFloat`` ground truth,
+    ``CohereVectorDBFloat.py:62,156``).  Ties by lower row (FAISS CMin heap)."""
+    S = Q.astype(np.float32) @ F.astype(np.float32).T
+    out = np.empty((Q.shape[0], k), dtype=np.int64)
+    idx = np.arange(F.shape[0])
+    for q in range(Q.shape[0]):
+        out[q] = np.lexsort((idx, -S[q]))[:k]
+    return out
+
+
+# --------------------------------------------------------------------------
+# Encoders (VectorDBInt{4,8,16}{,Global}); literal restatements
+# --------------------------------------------------------------------------
+def to_binary(x: np.ndarray) -> np.ndarray:
+    """``_to_binary``: packbits(x > np.mean(x)) -- ``VectorDBInt8Global.py:154-160``
+    (identical in ``VectorDBInt8.py:140-146``, ``VectorDBInt4.py:186-192``,
+    ``VectorDBInt4Global.py:190-196``, ``VectorDBInt16Global.py:154-160``,
+    ``VectorDBInt16.py:148-157`` where the mean of int16 is float64)."""
+    return np.packbits((x > np.mean(x)).astype(np.uint8))
+
+
+def to_binary_sign(x: np.ndarray) -> np.ndarray:
+    """Cohere ``ubinary`` emulation for synthetic corpora: packbits(x > 0).
+    (Matches the real ``db_cohere_enhanced`` codes vs ``db_cohere_float`` floats
+    on all but 2 of 1,024,000 bits)"""
+    return np.packbits((x > 0).astype(np.uint8))
+
+
+def quantize_int8_global(x: np.ndarray, limit: float) -> np.ndarray:
+    """``VectorDBInt8Global._quantize_to_int8`` (``VectorDBInt8Global.py:130-142``)."""
+    clipped = np.clip(x, -limit, limit)
+    scale = 127.0 / limit
+    scaled = np.round(clipped * scale)
+    return np.clip(scaled, -127, 127).astype(np.int8)
+
+
+def quantize_int16_global(x: np.ndarray, limit: float) -> np.ndarray:
+    """``VectorDBInt16Global._quantize_to_int16`` (``VectorDBInt16Global.py:130-142``)."""
+    clipped = np.clip(x, -limit, limit)
+    scale = 32767.0 / limit
+    scaled = np.round(clipped * scale)
+    return np.clip(scaled, -32767, 32767).astype(np.int16)
+
+
+def _pack_int4(scaled: np.ndarray) -> np.ndarray:
+    # nibble loop of VectorDBInt4.py:138-153 / VectorDBInt4Global.py:150-164
+    n = scaled.shape[0]
+    lp = (n + 1) // 2
+    out = np.zeros(lp, dtype=np.int8)
+    for i in range(lp):
+        a = int(scaled[2 * i]) + 8
+        b = int(scaled[2 * i + 1]) + 8 if 2 * i + 1 < n else 0
+        c = ((a & 0x0F) << 4) | (b & 0x0F)
+        if c > 127:
+            c -= 256
+        out[i] = np.int8(c)
+    return out
+
+
+def quantize_int4_global(x: np.ndarray, limit: float) -> np.ndarray:
+    """``VectorDBInt4Global._quantize_to_int4`` (``VectorDBInt4Global.py:129-164``).
+    Reproduces the reference bug: ``limit`` is ignored, the scale is the
+    per-vector 7/max|x|."""
+    mn = float(np.min(x))
+    mx = float(np.max(x))
+    if mx == mn:
+        return np.zeros((x.shape[0] + 1) // 2, dtype=np.int8)
+    scale = 7.0 / max(abs(mn), abs(mx))
+    scaled = np.clip(np.round(x * scale), -8, 7).astype(np.int8)
+    return _pack_int4(scaled)
+
+
+def quantize_int8_local(x: np.ndarray):
+    """``VectorDBInt8._quantize_to_int8`` (``VectorDBInt8.py:114-126``):
+    scale = 127/max(|min|,|max|) in float32, truncating ``astype(int8)``."""
+    mn = np.min(x)
+    mx = np.max(x)
+    if mx == mn:
+        return np.zeros_like(x, dtype=np.int8), mn, mx
+    scale = 127 / max(abs(mn), abs(mx))
+    return (x * scale).astype(np.int8), mn, mx
+
+
+def quantize_int4_local(x: np.ndarray):
+    """``VectorDBInt4._quantize_to_int4`` (``VectorDBInt4.py:116-154``)."""
+    mn = float(np.min(x))
+    mx = float(np.max(x))
+    if mx == mn:
+        return np.zeros((x.shape[0] + 1) // 2, dtype=np.int8), mn, mx
+    scale = 7.0 / max(abs(mn), abs(mx))
+    scaled = np.clip(np.round(x * scale), -8, 7).astype(np.int8)
+    return _pack_int4(scaled), mn, mx
+
+
+def dequantize_int8_global(q: np.ndarray, limit: float) -> np.ndarray:
+    """``VectorDBInt8Global._dequantize_int8`` (``:144-152``)."""
+    return q.astype(np.float32) * (limit / 127.0)
+
+
+def encode_batch(mode: str, X: np.ndarray, limit: float = 0.3):
+    """Row-wise application of one encoder; returns (codes, quantized, minmax|None)."""
+    X = np.asarray(X)
+    codes, qs, mm = [], [], []
+    for x in X:
+        if mode == "int8g":
+            qs.append(quantize_int8_global(x, limit)); codes.append(to_binary(x))
+        elif mode == "int16g":
+            qs.append(quantize_int16_global(x, limit)); codes.append(to_binary(x))
+        elif mode == "int4g":
+            qs.append(quantize_int4_global(x, limit)); codes.append(to_binary(x))
+        elif mode == "int8":
+            q, a, b = quantize_int8_local(x); qs.append(q); mm.append((a, b)); codes.append(to_binary(x))
+        elif mode == "int4":
+            q, a, b = quantize_int4_local(x); qs.append(q); mm.append((a, b)); codes.append(to_binary(x))
+        elif mode == "bin16":
+            codes.append(to_binary(x))
+        elif mode == "cohere":
+            qs.append(quantize_int8_global(x, limit)); codes.append(to_binary_sign(x))
+        else:
+            raise ValueError(mode)
+    codes = np.stack(codes) if codes else np.zeros((0, X.shape[1] // 8), np.uint8)
+    qs = np.stack(qs) if qs else None
+    mm = np.array(mm, dtype=np.float64) if mm else None
+    return codes, qs, mm

@@ -1,0 +1,384 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE's own code.
+
+Runs only in the survey/build container, where the reference checkout is
+mounted read-only at /root/reference (it never exists on the GPU box; the
+fixtures written here are what travel).  Nothing from the reference is copied:
+its modules are imported in place (bytecode writing disabled) with the two
+absent native dependencies stubbed:
+
+* ``faiss``    -> a module whose ``IndexBinaryIDMap2``/``IndexBinaryFlat`` are
+  the oracle's NumPy restatement (``oracle/oracle_np.py``);  FAISS itself is
+  not installed and not vendored, so Phase I in these fixtures is pinned to
+  the restated FAISS semantics (DESIGN.md "parity unpinned" note).
+* ``rocksdict`` -> ``Rdict = dict`` (a plain in-memory document store).
+
+The reference's methods then run UNMODIFIED:
+* the static encoders ``_quantize_to_*`` / ``_to_binary`` of all six
+  ``VectorDBInt{4,8,16}{,Global}`` classes  -> ``encoders.npz``;
+* ``CohereEnhancedVectorDB.search`` (Phases I-III, ``:227-322``) and
+  ``add_documents``/``remove_document`` (``:171-225,324-340``) with the HTTP
+  embedding call replaced by a table lookup -> ``search_synth.npz``;
+* the same ``search`` on the real 1000-document data persisted in the
+  reference (``db_cohere_enhanced/index.bin``: ubinary codes; ``docs/000009.sst``:
+  int8 vectors; ``db_cohere_float/index.faiss``: float32 vectors)
+  -> ``search_real.npz``.
+
+Safe loading: index.bin / index.faiss are raw FAISS binary formats read with
+``numpy.frombuffer``.  The SST values are pickles; they are NOT unpickled --
+``pickletools.genops`` (an opcode disassembler that constructs and executes
+nothing) is used to pull out the ``"doc"`` string and the raw 1024-byte int8
+payload.
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import io
+import os
+import pickletools
+import struct
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from oracle import oracle_np as O  # noqa: E402
+
+
+def _install_stubs():
+    faiss = types.ModuleType("faiss")
+
+    class _Flat:  # IndexBinaryFlat(d) placeholder: carries d only
+        def __init__(self, d):
+            self.d = d
+
+    faiss.IndexBinaryFlat = _Flat
+    faiss.IndexBinaryIDMap2 = lambda flat: O.IndexBinaryIDMap2(flat.d)
+    faiss.write_index_binary = lambda index, path: None
+    faiss.read_index_binary = lambda path: (_ for _ in ()).throw(RuntimeError("no faiss"))
+    sys.modules["faiss"] = faiss
+    rd = types.ModuleType("rocksdict")
+    rd.Rdict = dict
+    sys.modules["rocksdict"] = rd
+
+
+def _import_ref(name):
+    _install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    return __import__(name)
+
+
+# ---------------------------------------------------------------------------
+# 1. encoders
+# ---------------------------------------------------------------------------
+def make_encoder_inputs(d: int, rng) -> np.ndarray:
+    rows = []
+    for scale in (0.001, 0.02, 0.05, 0.1, 0.3, 1.0, 3.0):
+        for _ in range(6):
+            rows.append(rng.standard_normal(d) * scale)
+    v = rng.standard_normal(d)
+    rows.append(v / np.linalg.norm(v))                     # unit norm (Cohere-like)
+    rows.append(np.zeros(d))                                # constant zero
+    rows.append(np.full(d, 0.125))                          # constant non-zero
+    oh = np.zeros(d); oh[d // 3] = 0.7; rows.append(oh)     # one-hot
+    rows.append(np.linspace(-0.4, 0.4, d))                  # crosses +-limit
+    e = rng.standard_normal(d) * 0.2; e[::7] = 0.3; e[1::7] = -0.3; rows.append(e)  # exactly +-limit
+    # exact .5 ties after scaling for limit = 127/64 (scale 64) and for int4 (7/m = power of two)
+    t = (rng.integers(-120, 120, d) + 0.5) / 64.0; rows.append(t)
+    t4 = (rng.integers(-7, 7, d) + 0.5) / 8.0; t4[0] = 0.875; rows.append(t4)          # 7/m = 8
+    t4b = (rng.integers(-7, 7, d) + 0.5); t4b[0] = 7.0; rows.append(t4b / 1.0)   # m = 7 -> scale 1
+    # mean ties: half the entries equal to the mean
+    m = np.where(np.arange(d) % 2 == 0, 0.25, -0.25); rows.append(m)
+    return np.asarray(rows, dtype=np.float32)
+
+
+def gen_encoders(out_path: str):
+    rng = np.random.default_rng(20250218)
+    I8G = _import_ref("VectorDBInt8Global").VectorDBInt8Global
+    I16G = _import_ref("VectorDBInt16Global").VectorDBInt16Global
+    I4G = _import_ref("VectorDBInt4Global").VectorDBInt4Global
+    I8 = _import_ref("VectorDBInt8").VectorDBInt8
+    I4 = _import_ref("VectorDBInt4").VectorDBInt4
+    I16 = _import_ref("VectorDBInt16").VectorDBInt16
+    res = {}
+    for d in (1024, 384):
+        X = make_encoder_inputs(d, rng)
+        res[f"x_{d}"] = X
+        for limit, tag in ((0.3, "l03"), (0.1, "l01"), (1.0, "l10"), (127.0 / 64.0, "ltie")):
+            res[f"int8g_{tag}_{d}"] = np.stack([I8G._quantize_to_int8(x, limit) for x in X])
+            res[f"int16g_{tag}_{d}"] = np.stack([I16G._quantize_to_int16(x, limit) for x in X])
+            res[f"int4g_{tag}_{d}"] = np.stack([I4G._quantize_to_int4(x, limit) for x in X])
+            res[f"limit_{tag}"] = np.float64(limit)
+        q8 = [I8._quantize_to_int8(x) for x in X]
+        res[f"int8_{d}"] = np.stack([a for a, _, _ in q8])
+        res[f"int8_minmax_{d}"] = np.array([(float(b), float(c)) for _, b, c in q8], dtype=np.float64)
+        q4 = [I4._quantize_to_int4(x) for x in X]
+        res[f"int4_{d}"] = np.stack([a for a, _, _ in q4])
+        res[f"int4_minmax_{d}"] = np.array([(b, c) for _, b, c in q4], dtype=np.float64)
+        for name, cls in (("int8g", I8G), ("int16g", I16G), ("int4g", I4G), ("int8", I8), ("int4", I4)):
+            res[f"bin_{name}_{d}"] = np.stack([cls._to_binary(x) for x in X])
+        # VectorDBInt16 receives int16 vectors from its service (:92-146)
+        X16 = rng.integers(-32767, 32768, size=(24, d)).astype(np.int16)
+        X16[0] = 0; X16[1] = 5; X16[2, ::2] = 100; X16[2, 1::2] = -100
+        X16[3] = (rng.integers(-3, 4, d)).astype(np.int16)
+        res[f"x16_{d}"] = X16
+        res[f"bin16_{d}"] = np.stack([I16._to_binary(x) for x in X16])
+        # sanity: the oracle restatement reproduces the reference bit-for-bit
+        for x, ref in zip(X, res[f"int8g_l03_{d}"]):
+            assert np.array_equal(O.quantize_int8_global(x, 0.3), ref)
+        for x, ref in zip(X, res[f"bin_int8g_{d}"]):
+            assert np.array_equal(O.to_binary(x), ref)
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path, sorted(res)[:6], "...")
+
+
+# ---------------------------------------------------------------------------
+# 2. three-phase search through the reference's own CohereEnhancedVectorDB
+# ---------------------------------------------------------------------------
+def _ref_db(doc_lookup: dict, query_lookup: dict):
+    CE = _import_ref("CohereEnhancedVectorDB").CohereEnhancedVectorDB
+    db = object.__new__(CE)            # skip __init__ (env vars / folders)
+    db.embedding_dim = 1024
+    db.model = "embed-english-v3.0"
+    db.folder = "/nonexistent"
+    db.config = {"model": db.model}
+    db.index = O.IndexBinaryIDMap2(1024)
+    db.doc_db = {}
+
+    def _get_embeddings(texts, input_type, embedding_types):
+        if input_type == "search_query":
+            f, b = query_lookup[texts[0]]
+            return {"float": [f.tolist()], "ubinary": [b.tolist()]}
+        return {"int8": [doc_lookup[t][0].tolist() for t in texts],
+                "ubinary": [doc_lookup[t][1].tolist() for t in texts]}
+
+    db._get_embeddings = _get_embeddings
+    return db
+
+
+def search_table(db, QF, QB, k, osb, osi, query_lookup):
+    nq = QF.shape[0]
+    out = {}
+    ids = np.full((nq, k), -1, np.int64); ham = np.full((nq, k), -1, np.int64)
+    bn = np.full((nq, k), np.nan); cs = np.full((nq, k), np.nan); cnt = np.zeros(nq, np.int64)
+    for j in range(nq):
+        query_lookup[f"q{j}"] = (QF[j], QB[j])
+        res = db.search(f"q{j}", k=k, binary_oversample=osb, int8_oversample=osi)
+        cnt[j] = len(res)
+        for r, h in enumerate(res):
+            ids[j, r] = h["doc_id"]; ham[j, r] = h["score_hamming"]
+            bn[j, r] = h["score_binary"]; cs[j, r] = h["score_cosine"]
+    out.update(ids=ids, ham=ham, bin=bn, cos=cs, cnt=cnt)
+    return out
+
+
+def synth_corpus(rng, n, d=1024, nclusters=64, sigma=None):
+    if sigma is None:
+        sigma = 0.6 / np.sqrt(d)
+    C = rng.standard_normal((nclusters, d)) / np.sqrt(d)
+    c = rng.integers(0, nclusters, n)
+    F = C[c] + sigma * rng.standard_normal((n, d))
+    F /= np.linalg.norm(F, axis=1, keepdims=True)
+    return F.astype(np.float32)
+
+
+def gen_search_synth(out_path: str):
+    rng = np.random.default_rng(7)
+    N = 1500
+    F = synth_corpus(rng, N)
+    # planted exact duplicates (identical float -> identical codes and int8): ties in every phase
+    for a, b in ((10, 700), (11, 701), (11, 702), (500, 1499)):
+        F[b] = F[a]
+    Q8 = np.stack([O.quantize_int8_global(x, 0.1) for x in F])
+    QB = np.stack([O.to_binary_sign(x) for x in F])
+    # duplicated code with a different int8 vector (Phase I tie, Phase II tie, Phase III split)
+    QB[900] = QB[20]
+    # a zero int8 vector -> -inf cosine (norm == 0 branch, :309-310)
+    Q8[1234] = 0
+    ids = np.arange(N, dtype=np.int64) * 3 + 1000           # external ids != rows
+    nq = 24
+    src = rng.integers(0, N, nq)
+    src[0] = 10; src[1] = 11; src[2] = 20; src[3] = 1234
+    QF = F[src] + (0.3 / np.sqrt(1024)) * rng.standard_normal((nq, 1024)).astype(np.float32)
+    QF[0] = F[10]                                             # exact duplicate query
+    QF /= np.linalg.norm(QF, axis=1, keepdims=True)
+    QF = QF.astype(np.float32)
+    QBq = np.stack([O.to_binary_sign(x) for x in QF])
+
+    docs = {f"t{i}": (Q8[i], QB[i]) for i in range(N)}
+    qlk = {}
+    db = _ref_db(docs, qlk)
+    texts = [f"t{i}" for i in range(N)]
+    db.add_documents([int(x) for x in ids], texts, batch_size=64, save=False)   # :171-225
+    res = {"int8": Q8, "codes": QB, "ids": ids, "qf": QF, "qb": QBq}
+    for tag, (k, osb, osi) in {"k10": (10, 10, 3), "k50": (50, 10, 3), "k7": (7, 4, 2)}.items():
+        r = search_table(db, QF, QBq, k, osb, osi, qlk)
+        for kk, v in r.items():
+            res[f"{tag}_{kk}"] = v
+        res[f"{tag}_params"] = np.array([k, osb, osi])
+
+    # small corpus (k*os > ntotal) + remove/re-add path (dedupe :190-192, remove_ids :334)
+    db2 = _ref_db(docs, qlk)
+    small = [5, 6, 7, 8, 9, 10, 700, 11, 701, 702, 20, 900, 1234, 33, 34, 35, 36, 37, 38, 39]
+    db2.add_documents(small, [f"t{i}" for i in small], batch_size=8, save=False)
+    db2.remove_document(8, save=False)
+    db2.remove_document(36, save=False)
+    db2.add_documents([36, 40, 7], ["t36", "t40", "t999"], batch_size=64, save=False)  # 7 re-added with t999
+    res["small_rows_ids"] = db2.index.id_map.copy()
+    res["small_codes"] = db2.index.xb.copy()
+    res["small_int8"] = np.stack([np.asarray(db2.doc_db[str(int(e))]["int8"], np.int8) for e in db2.index.id_map])
+    r = search_table(db2, QF, QBq, 10, 10, 3, qlk)
+    for kk, v in r.items():
+        res[f"small_{kk}"] = v
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
+
+
+# ---------------------------------------------------------------------------
+# 3. real 1000-doc Cohere data persisted in the reference
+# ---------------------------------------------------------------------------
+def read_ibm2(path):
+    b = open(path, "rb").read()
+    assert b[:4] == b"IBM2" and b[25:29] == b"IBxF"
+    d, cs, nt = struct.unpack("<iiq", b[4:20])
+    off = 50
+    nb, = struct.unpack("<q", b[off:off + 8]); off += 8
+    xb = np.frombuffer(b, np.uint8, nb, off).reshape(nt, cs).copy(); off += nb
+    ni, = struct.unpack("<q", b[off:off + 8]); off += 8
+    idm = np.frombuffer(b, "<i8", ni, off).copy()
+    return xb, idm
+
+
+def read_ixmp_flat(path):
+    b = open(path, "rb").read()
+    assert b[:4] == b"IxMp" and b[37:41] == b"IxFI"
+    d, = struct.unpack("<i", b[4:8]); nt, = struct.unpack("<q", b[8:16])
+    off = 41 + 33
+    nx, = struct.unpack("<q", b[off:off + 8]); off += 8
+    xb = np.frombuffer(b, "<f4", nx, off).reshape(nt, d).copy(); off += 4 * nx
+    ni, = struct.unpack("<q", b[off:off + 8]); off += 8
+    idm = np.frombuffer(b, "<i8", ni, off).copy()
+    return xb, idm
+
+
+def _varint(b, p):
+    r = s = 0
+    while True:
+        c = b[p]; p += 1
+        r |= (c & 0x7F) << s; s += 7
+        if c < 0x80:
+            return r, p
+
+
+def _scan_pickle(blob):
+    """Extract ('doc' text, int8 bytes) from a protocol-4 pickle WITHOUT executing it."""
+    strings, payload = [], None
+    for op, arg, _ in pickletools.genops(io.BytesIO(blob)):
+        if op.name in ("SHORT_BINUNICODE", "BINUNICODE"):
+            strings.append(arg)
+        elif op.name in ("BINBYTES", "SHORT_BINBYTES", "BINBYTES8") and len(arg) > 1:
+            payload = arg
+        elif op.name == "STOP":
+            break
+    doc = strings[strings.index("doc") + 1]
+    return doc, np.frombuffer(payload, np.int8).copy()
+
+
+def read_sst_records(path):
+    """Walk the uncompressed data blocks of a RocksDB SST; return {id: (doc, int8)}."""
+    b = open(path, "rb").read()
+    recs, best = {}, {}
+    starts = []
+    p = 0
+    marker = b"\x06\x80\x04\x95"
+    while True:
+        q = b.find(marker, p)
+        if q < 0:
+            break
+        starts.append(q); p = q + 1
+    key = b""
+    pos = 0
+    for q in starts:
+        if q < pos:
+            continue
+        # try parsing an entry that ends its key exactly at q, walking back a few bytes
+        ok = False
+        for back in range(3, 40):
+            h = q - back
+            if h < 0:
+                break
+            try:
+                sh, h2 = _varint(b, h); un, h3 = _varint(b, h2); vl, h4 = _varint(b, h3)
+            except IndexError:
+                continue
+            if h4 + un == q and sh <= len(key) and un >= 9:
+                delta = b[h4:q]
+                user, trailer = delta[:-8], delta[-8:]
+                if trailer[0] != 1:            # kTypeValue
+                    continue
+                if sh == 0 and not user.startswith(b"\x02"):
+                    continue
+                digits = user[1:] if sh == 0 else user
+                if not all(48 <= c <= 57 for c in digits):
+                    continue
+                key = key[:sh] + delta
+                val = b[q:q + vl]
+                ok = True
+                pos = q + vl
+                break
+        if not ok:
+            continue
+        ukey, trailer = key[:-8], key[-8:]
+        seq = int.from_bytes(trailer, "little") >> 8
+        assert ukey[:1] == b"\x02"
+        i = int(ukey[1:].decode())
+        doc, v = _scan_pickle(val[1:])
+        if i not in best or seq > best[i]:
+            best[i] = seq; recs[i] = (doc, v)
+    return recs
+
+
+def gen_search_real(out_path: str):
+    xb, idm = read_ibm2(os.path.join(REF, "db_cohere_enhanced/index.bin"))
+    F, fid = read_ixmp_flat(os.path.join(REF, "db_cohere_float/index.faiss"))
+    recs = read_sst_records(os.path.join(REF, "db_cohere_enhanced/docs/000009.sst"))
+    assert sorted(recs) == list(range(1000)), len(recs)
+    assert np.array_equal(idm, np.arange(1000)) and np.array_equal(fid, np.arange(1000))
+    I8 = np.stack([recs[i][1] for i in range(1000)])
+    texts = [recs[i][0] for i in range(1000)]
+    docs = {f"d{i}": (I8[i], xb[i]) for i in range(1000)}
+    qlk = {}
+    db = _ref_db(docs, qlk)
+    db.add_documents(list(range(1000)), [f"d{i}" for i in range(1000)], batch_size=64, save=False)
+    qsrc = np.arange(0, 1000, 10)
+    QF = F[qsrc].astype(np.float32)
+    QB = np.stack([O.to_binary_sign(x) for x in QF])
+    res = {"codes": xb, "int8": I8, "qsrc": qsrc, "qf": QF, "qb": QB,
+           "gt_float_top10": O.float_ip_topk(F, QF, 10),
+           "sign_bits_mismatch": np.int64((np.stack([O.to_binary_sign(x) for x in F]) != xb).sum())}
+    r = search_table(db, QF, QB, 10, 10, 3, qlk)
+    for kk, v in r.items():
+        res[f"k10_{kk}"] = v
+    r = search_table(db, QF, QB, 50, 10, 3, qlk)
+    for kk, v in r.items():
+        res[f"k50_{kk}"] = v
+    rec = np.mean([len(set(a) & set(b)) / 10.0 for a, b in zip(res["k10_ids"], res["gt_float_top10"])])
+    res["recall10"] = np.float64(rec)
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path, "recall@10 vs float32 =", rec)
+
+
+if __name__ == "__main__":
+    if not os.path.isdir(REF):
+        sys.exit("reference checkout not mounted; fixtures are generated in the build container only")
+    gen_encoders(os.path.join(HERE, "encoders.npz"))
+    gen_search_synth(os.path.join(HERE, "search_synth.npz"))
+    gen_search_real(os.path.join(HERE, "search_real.npz"))

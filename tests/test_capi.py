@@ -1,0 +1,66 @@
+"""The C ABI library loads and exports every symbol include/vrq.h declares; argument
+validation paths that never touch a GPU.  CPU only."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from vectorragquantization_amd import _native as N
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "vrq.h")
+
+
+def declared():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(vrq_\w+)\s*\(", src, re.M)))
+
+
+def test_header_and_binding_agree():
+    names = declared()
+    assert len(names) >= 11
+    assert sorted(N.SIGNATURES) == names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.load()
+    raw = C.CDLL(N.lib_path())
+    for name in declared():
+        assert hasattr(raw, name), name
+    assert lib.vrq_abi_version() == 1
+    assert lib.vrq_strerror(N.VRQ_EUNSUPPORTED) == b"unsupported shape"
+
+
+def test_workspace_sizes():
+    lib = N.load()
+    # nq * nchunks * K * 8 bytes; deterministic in the call shape
+    ws = lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 100)
+    assert ws > 0 and ws % (1024 * 100 * 8) == 0
+    assert ws == lib.vrq_hamming_topk_workspace_size(1_000_000, 128, 1024, 100)
+    assert lib.vrq_search3_workspace_size(1000, 512, 1, 10) == 0      # dim unsupported
+    assert lib.vrq_hamming_topk_workspace_size(10, 128, 1, 2000) == 0  # K > 1024
+    n = 100_000_000
+    per_q = lib.vrq_hamming_topk_workspace_size(n, 128, 1, 100) // (100 * 8)
+    assert 1 <= per_q <= 4096
+
+
+@pytest.mark.parametrize("call,expect", [
+    (lambda L: L.vrq_encode(99, None, 1, 1024, 0.3, None, None, None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_encode(0, None, -1, 1024, 0.3, None, None, None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_encode(0, None, 1, 1020, 0.3, None, None, None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_encode(0, None, 1, 1024, 0.0, None, None, None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_encode(0, None, 0, 1024, 0.3, None, None, None, None), N.VRQ_OK),
+    (lambda L: L.vrq_search3(None, None, None, None, 10, 512, 0, None, None, 1, 1, 1, 1, 0,
+                             C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8),
+                             None, 0, None), N.VRQ_EUNSUPPORTED),
+    (lambda L: L.vrq_search3(None, None, None, None, 10, 1024, 0, None, None, 1, 1, 2000, 1, 0,
+                             C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8),
+                             None, 0, None), N.VRQ_EUNSUPPORTED),
+    (lambda L: L.vrq_hamming_topk(None, 10, 128, 0, None, 1, 1, None, None, None, 0, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_rescore_binary(None, 1, 512, None, 1, None, 1, None, None), N.VRQ_EUNSUPPORTED),
+    (lambda L: L.vrq_merge_shards(0, 1, 1, None, None, None, None, None, 1, 1, None, None, None, None, None,
+                                  None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_int8_row_norms(None, -1, 1024, None, None), N.VRQ_EINVAL),
+])
+def test_argument_validation(call, expect):
+    assert call(N.load()) == expect

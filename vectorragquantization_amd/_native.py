@@ -1,0 +1,109 @@
+"""ctypes binding of libvrq.so (include/vrq.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot
+be loaded, every call raises ``VrqNativeError`` -- tests on a GPU box therefore
+fail loudly instead of silently running something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from . import _build
+
+VRQ_OK = 0
+VRQ_EINVAL = -1
+VRQ_EHIP = -2
+VRQ_EUNSUPPORTED = -3
+VRQ_EWORKSPACE = -4
+
+VRQ_SEARCH_PHASE1_ONLY = 1
+VRQ_SEARCH_SHARD = 2
+
+ENC_MODES = {
+    "int8g": 0,   # VectorDBInt8Global
+    "int16g": 1,  # VectorDBInt16Global
+    "int4g": 2,   # VectorDBInt4Global (limit ignored, reference bug)
+    "int8": 3,    # VectorDBInt8
+    "int4": 4,    # VectorDBInt4
+    "bin16": 5,   # VectorDBInt16._to_binary
+    "cohere": 6,  # synthetic Cohere provider (int8 global + sign bits)
+}
+
+# name -> (restype, argtypes); mirrors include/vrq.h
+_P, _I32, _I64, _SZ, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t, C.c_double
+SIGNATURES = {
+    "vrq_abi_version": (C.c_int, []),
+    "vrq_strerror": (C.c_char_p, [C.c_int]),
+    "vrq_hamming_topk_workspace_size": (_SZ, [_I64, _I32, _I32, _I32]),
+    "vrq_hamming_topk": (C.c_int, [_P, _I64, _I32, _I64, _P, _I32, _I32, _P, _P, _P, _SZ, _P]),
+    "vrq_search3_workspace_size": (_SZ, [_I64, _I32, _I32, _I32]),
+    "vrq_search3": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _P, _I32, _I32, _I32, _I32, _I32,
+                              _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "vrq_search3_scan": (C.c_int, [_P, _I64, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "vrq_search3_finish": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _I32, _I32,
+                                     _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "vrq_merge_shards": (C.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "vrq_rescore_binary": (C.c_int, [_P, _I32, _I32, _P, _I64, _P, _I32, _P, _P]),
+    "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),
+    "vrq_encode": (C.c_int, [_I32, _P, _I64, _I32, _D, _P, _P, _P, _P]),
+    "vrq_int8_row_norms": (C.c_int, [_P, _I64, _I32, _P, _P]),
+}
+
+
+class VrqNativeError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return os.environ.get("VRQ_LIB", _build.LIB)
+
+
+def load():
+    """Load (building first if needed and possible) libvrq.so; raise on failure."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not os.path.exists(path) or (path == _build.LIB and not _build.up_to_date()):
+            try:
+                _build.build()
+            except Exception as e:  # no hipcc on this host and no prebuilt library
+                if not os.path.exists(path):
+                    raise VrqNativeError(f"libvrq.so missing and cannot be built: {e}") from e
+        try:
+            lib = C.CDLL(path)
+        except OSError as e:
+            raise VrqNativeError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.vrq_abi_version() != 1:
+            raise VrqNativeError("libvrq ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != VRQ_OK:
+        msg = load().vrq_strerror(rc).decode()
+        raise VrqNativeError(f"{what} failed: {msg} ({rc})")
+
+
+def ptr(t) -> int:
+    """Raw device pointer of a torch tensor (None -> NULL)."""
+    return 0 if t is None else int(t.data_ptr())
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return int(torch.cuda.current_stream(device).cuda_stream)

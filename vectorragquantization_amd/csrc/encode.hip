@@ -1,0 +1,322 @@
+// encode.hip -- K6: the VectorDBInt{4,8,16}{,Global} scalar-quantise + packbits
+// encode path, and K7: float64 int8 row norms.  One wave per vector.
+//
+// Bit-exactness notes (NumPy 2.x semantics of the reference expressions):
+//  * _to_binary: packbits(x > np.mean(x)), MSB first.  np.mean(float32) is NumPy's
+//    pairwise summation (8 strided accumulators per <=128-element leaf, fixed
+//    combine tree, then / n with one rounding to float32).  The leaf / tree
+//    structure depends only on n; the host builds it (PwPlan) and the kernel
+//    replays it: 8 lanes per leaf accumulate their column sequentially, a 3-step
+//    butterfly reproduces ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), one lane adds the
+//    leaf's tail and one lane folds the leaves in the recursion's order.  Built
+//    with -ffp-contract=off so no add is fused.
+//  * scalar scales are Python floats cast to float32 at the multiply (weak
+//    scalars): scale32 = (float)(c / limit) in double, which equals the
+//    correctly rounded float32 quotient.  np.round = rintf (half to even);
+//    .astype(int8) from float truncates (VectorDBInt8.py:126).
+//  * VectorDBInt4Global ignores its limit (reference bug, reproduced).
+#include "vrq_internal.h"
+
+namespace vrq {
+
+constexpr int MAX_DIM = 8192;
+constexpr int MAX_LEAVES = 128;
+constexpr int MAX_OPS = 2 * MAX_LEAVES;
+
+struct PwPlan {
+  int nleaves;
+  int nops;
+  int16_t start[MAX_LEAVES];
+  int16_t len[MAX_LEAVES];
+  int16_t ops[MAX_OPS];  // postfix: >= 0 push leaf sum, -1 add the top two
+};
+
+static void pw_build(int s, int n, PwPlan* p) {
+  if (n <= 128) {
+    p->start[p->nleaves] = (int16_t)s;
+    p->len[p->nleaves] = (int16_t)n;
+    p->ops[p->nops++] = (int16_t)p->nleaves++;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  pw_build(s, n2, p);
+  pw_build(s + n2, n - n2, p);
+  p->ops[p->nops++] = -1;
+}
+
+// NumPy pairwise float32 sum of x[0..n) staged in LDS; result valid in all lanes.
+__device__ float pairwise_sum_f32(const float* x, const PwPlan& P, float* leafsum) {
+  const int l = lane_id(), g = l >> 3, j = l & 7;
+  for (int b = 0; b < P.nleaves; b += 8) {
+    const int li = b + g;
+    float r = 0.f;
+    int m = 0, s = 0;
+    if (li < P.nleaves) {
+      s = P.start[li];
+      m = P.len[li];
+      if (m >= 8) {
+        r = x[s + j];
+        for (int i = 8; i < m - (m % 8); i += 8) r += x[s + i + j];
+      }
+    }
+    // tree over the 8 accumulators of the leaf (lanes 8g..8g+7)
+    float t = r + __shfl_xor(r, 1, WAVE);
+    t = t + __shfl_xor(t, 2, WAVE);
+    t = t + __shfl_xor(t, 4, WAVE);
+    if (j == 0 && li < P.nleaves) {
+      float res;
+      int i;
+      if (m >= 8) {
+        res = t;
+        i = m - (m % 8);
+      } else {
+        res = 0.f;
+        i = 0;
+      }
+      for (; i < m; ++i) res += x[s + i];
+      leafsum[li] = res;
+    }
+  }
+  __syncthreads();
+  float out = 0.f;
+  if (l == 0) {
+    float* st = leafsum + MAX_LEAVES;  // LDS stack (no scratch)
+    int sp = 0;
+    for (int o = 0; o < P.nops; ++o) {
+      const int op = P.ops[o];
+      if (op >= 0) {
+        st[sp++] = leafsum[op];
+      } else {
+        const float rgt = st[--sp];
+        const float lft = st[--sp];
+        st[sp++] = lft + rgt;
+      }
+    }
+    out = st[0];
+  }
+  return __shfl(out, 0, WAVE);
+}
+
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+template <int MODE>
+__global__ __launch_bounds__(64) void encode_kernel(const void* __restrict__ xin, int64_t n, int dim, double limit,
+                                                    uint8_t* __restrict__ codes, void* __restrict__ qout,
+                                                    double* __restrict__ minmax, PwPlan P) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // dim floats + leaf sums
+  float* leafsum = xs + dim;
+  const int64_t v = blockIdx.x;
+  if (v >= n) return;
+  const int l = lane_id();
+  const int ngroups = dim / 8;
+  uint8_t* crow = codes + v * ngroups;
+
+  if constexpr (MODE == VRQ_ENC_BIN_INT16) {
+    // VectorDBInt16._to_binary: float64 mean of int16 (exact sum), x > mean
+    const int16_t* x = reinterpret_cast<const int16_t*>(xin) + v * dim;
+    int64_t s = 0;
+    for (int i = l; i < dim; i += WAVE) s += x[i];
+    s = wave_sum_i64(s);
+    const double mean = (double)s / (double)dim;
+    for (int gi = l; gi < ngroups; gi += WAVE) {
+      uint32_t byte = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) byte |= ((double)x[8 * gi + k] > mean ? 1u : 0u) << (7 - k);
+      crow[gi] = (uint8_t)byte;
+    }
+    return;
+  } else {
+    const float* x = reinterpret_cast<const float*>(xin) + v * dim;
+    for (int i = 4 * l; i < dim; i += 4 * WAVE) *reinterpret_cast<float4*>(xs + i) = *reinterpret_cast<const float4*>(x + i);
+    __syncthreads();
+    float mean = 0.f;
+    if constexpr (MODE != VRQ_ENC_COHERE) {
+      const float s = pairwise_sum_f32(xs, P, leafsum);
+      mean = (float)((double)s / (double)dim);  // np.float32(sum) / np.intp(n) -> float32
+    }
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    if constexpr (MODE == VRQ_ENC_INT4_GLOBAL || MODE == VRQ_ENC_INT8_LOCAL || MODE == VRQ_ENC_INT4_LOCAL) {
+      for (int i = l; i < dim; i += WAVE) {
+        mn = fminf(mn, xs[i]);
+        mx = fmaxf(mx, xs[i]);
+      }
+#pragma unroll
+      for (int m = 1; m < WAVE; m <<= 1) {
+        mn = fminf(mn, __shfl_xor(mn, m, WAVE));
+        mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
+      }
+      if constexpr (MODE != VRQ_ENC_INT4_GLOBAL) {
+        if (l == 0) {
+          minmax[2 * v] = (double)mn;
+          minmax[2 * v + 1] = (double)mx;
+        }
+      }
+    }
+    const float am = fmaxf(fabsf(mn), fabsf(mx));
+    const bool flat = (mx == mn);
+    float scale = 0.f, lim = 0.f;
+    if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
+      lim = (float)limit;
+      scale = (float)(127.0 / limit);
+    } else if constexpr (MODE == VRQ_ENC_INT16_GLOBAL) {
+      lim = (float)limit;
+      scale = (float)(32767.0 / limit);
+    } else if constexpr (MODE == VRQ_ENC_INT8_LOCAL) {
+      scale = flat ? 0.f : (float)(127.0 / (double)am);
+    } else {
+      scale = flat ? 0.f : (float)(7.0 / (double)am);
+    }
+    for (int gi = l; gi < ngroups; gi += WAVE) {
+      float e[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = xs[8 * gi + k];
+      uint32_t byte = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool bit = (MODE == VRQ_ENC_COHERE) ? (e[k] > 0.f) : (e[k] > mean);
+        byte |= (bit ? 1u : 0u) << (7 - k);
+      }
+      crow[gi] = (uint8_t)byte;
+      if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
+        uint32_t w[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float y = clampf(rintf(clampf(e[k], -lim, lim) * scale), -127.f, 127.f);
+          w[k >> 2] |= ((uint32_t)(uint8_t)(int8_t)(int)y) << (8 * (k & 3));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(qout) + v * dim + 8 * gi) = make_uint2(w[0], w[1]);
+      } else if constexpr (MODE == VRQ_ENC_INT16_GLOBAL) {
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float y = clampf(rintf(clampf(e[k], -lim, lim) * scale), -32767.f, 32767.f);
+          w[k >> 1] |= ((uint32_t)(uint16_t)(int16_t)(int)y) << (16 * (k & 1));
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<int16_t*>(qout) + v * dim + 8 * gi) =
+            make_uint4(w[0], w[1], w[2], w[3]);
+      } else if constexpr (MODE == VRQ_ENC_INT8_LOCAL) {
+        uint32_t w[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int y = flat ? 0 : (int)(e[k] * scale);  // astype(int8): truncation toward zero
+          w[k >> 2] |= ((uint32_t)(uint8_t)(int8_t)y) << (8 * (k & 3));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(qout) + v * dim + 8 * gi) = make_uint2(w[0], w[1]);
+      } else {  // int4 (global: limit ignored; local): nibble pairs, high = even index
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          uint32_t byte4 = 0;
+          if (!flat) {
+            const int a = (int)clampf(rintf(e[k] * scale), -8.f, 7.f) + 8;
+            const int b = (int)clampf(rintf(e[k + 1] * scale), -8.f, 7.f) + 8;
+            byte4 = (uint32_t)(((a & 0x0f) << 4) | (b & 0x0f));
+          }
+          w |= byte4 << (8 * (k >> 1));
+        }
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + v * (dim / 2) + 4 * gi) = w;
+      }
+    }
+  }
+}
+
+// K7: ||x8 row||_2 in float64 from the exact integer sum of squares.
+__global__ __launch_bounds__(256) void int8_norms_kernel(const int8_t* __restrict__ x8, int64_t n, int dim,
+                                                         double* __restrict__ out) {
+  const int64_t v = ((int64_t)blockIdx.x * 256 + threadIdx.x) / WAVE;
+  if (v >= n) return;
+  const int l = lane_id();
+  const int8_t* r = x8 + v * dim;
+  int64_t s = 0;
+  if ((dim & 15) == 0) {
+    for (int i = 16 * l; i < dim; i += 16 * WAVE) {
+      const int4 raw = *reinterpret_cast<const int4*>(r + i);
+      const int32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int32_t e = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+        s += e * e;
+      }
+    }
+  } else {
+    for (int i = l; i < dim; i += WAVE) s += (int32_t)r[i] * (int32_t)r[i];
+  }
+  s = wave_sum_i64(s);
+  if (l == 0) out[v] = sqrt((double)s);
+}
+
+}  // namespace vrq
+
+using namespace vrq;
+
+extern "C" {
+
+int vrq_abi_version(void) { return VRQ_ABI_VERSION; }
+
+const char* vrq_strerror(int code) {
+  switch (code) {
+    case VRQ_OK: return "ok";
+    case VRQ_EINVAL: return "invalid argument";
+    case VRQ_EHIP: return "HIP runtime error";
+    case VRQ_EUNSUPPORTED: return "unsupported shape";
+    case VRQ_EWORKSPACE: return "workspace too small";
+    default: return "unknown vrq error";
+  }
+}
+
+int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit, uint8_t* codes, void* q,
+               double* minmax, void* stream) {
+  VRQ_CHECK_ARG(n >= 0 && dim > 0 && (dim % 8) == 0);
+  if (dim > MAX_DIM || (dim % 4) != 0) return VRQ_EUNSUPPORTED;
+  VRQ_CHECK_ARG(mode >= VRQ_ENC_INT8_GLOBAL && mode <= VRQ_ENC_COHERE);
+  const bool global_mode = mode == VRQ_ENC_INT8_GLOBAL || mode == VRQ_ENC_INT16_GLOBAL || mode == VRQ_ENC_COHERE;
+  if (global_mode) VRQ_CHECK_ARG(limit > 0.0);
+  if (n == 0) return VRQ_OK;
+  VRQ_CHECK_ARG(x && codes);
+  if (mode != VRQ_ENC_BIN_INT16) VRQ_CHECK_ARG(q);
+  if (mode == VRQ_ENC_INT8_LOCAL || mode == VRQ_ENC_INT4_LOCAL) VRQ_CHECK_ARG(minmax);
+  PwPlan P{};
+  pw_build(0, dim, &P);
+  if (P.nleaves > MAX_LEAVES) return VRQ_EUNSUPPORTED;
+  const size_t lds = sizeof(float) * (dim + 2 * MAX_LEAVES);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)n), block(64);
+  switch (mode) {
+    case VRQ_ENC_INT8_GLOBAL:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    case VRQ_ENC_INT16_GLOBAL:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    case VRQ_ENC_INT4_GLOBAL:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    case VRQ_ENC_INT8_LOCAL:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    case VRQ_ENC_INT4_LOCAL:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    case VRQ_ENC_BIN_INT16:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_BIN_INT16>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+    default:
+      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_COHERE>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
+      break;
+  }
+  VRQ_LAUNCH_CHECK();
+  return VRQ_OK;
+}
+
+int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, void* stream) {
+  VRQ_CHECK_ARG(n >= 0 && dim > 0);
+  if (n == 0) return VRQ_OK;
+  VRQ_CHECK_ARG(x8 && out);
+  const int64_t blocks = (n * WAVE + 255) / 256;
+  hipLaunchKernelGGL(int8_norms_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x8, n, dim, out);
+  VRQ_LAUNCH_CHECK();
+  return VRQ_OK;
+}
+
+}  // extern "C"

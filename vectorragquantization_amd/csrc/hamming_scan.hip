@@ -1,0 +1,338 @@
+// hamming_scan.hip -- K1: Phase-I exhaustive Hamming scan with per-chunk exact top-K.
+//
+// Replaces FAISS IndexBinaryFlat::search -> hammings_knn_hc (called from
+// CohereEnhancedVectorDB.py:268).  FAISS semantics: a max-heap ordered by
+// (dist, id) that admits a row only if dist < heap_top while rows arrive in
+// increasing index, i.e. the result is the K smallest rows under the
+// lexicographic (dist asc, row asc) order.  Here every wave scans one
+// contiguous CHUNK of rows for QG queries and keeps, per query, the exact top-K
+// of its chunk under that same order; K2 (select_rescore.hip) merges the chunk
+// lists.  The union of chunk top-Ks contains the global top-K, and the merge
+// is exact, so the final order is FAISS's.
+//
+// gfx950 mapping (one wave = one workgroup = one (chunk, query-group)):
+//  * corpus rows stream HBM -> LDS with global_load_lds_dwordx4 (LDS-DMA, 1 KiB
+//    per wave-instruction, fully coalesced); the per-lane SOURCE address is
+//    pre-swizzled so that the row-per-lane ds_read_b128 that follows is
+//    bank-conflict-free (linear LDS destination, swizzled source, same XOR on
+//    the read).  NBUF tiles in flight per wave.
+//  * each lane owns one row (CB/4 dwords in VGPRs); query dwords are
+//    wave-uniform and come from scalar loads (SGPR operands of v_xor_b32), so
+//    the distance of one (query,row) pair costs CB/4 v_xor + CB/4 v_bcnt
+//    (v_bcnt_u32_b32 accumulates) and nothing else.
+//  * top-K per query: a 32-bit LDS key (dist << 20 | chunk-local row) list of
+//    capacity CAP >= K + 64 and a wave-uniform threshold; a row is appended iff
+//    key < tau (ballot + mbcnt compaction).  When the list would overflow it is
+//    sorted by a wave-level bitonic network in registers (shuffles for strides
+//    < 64, register swaps above) and cut to K; tau = K-th key.
+//  * blockIdx -> (chunk, query group) is XCD-aware: blocks that share an XCD
+//    (b % 8) get consecutive linear ids, i.e. the same chunk for different
+//    query groups, so re-reads of a chunk hit that XCD's L2.
+#include "vrq_internal.h"
+#include "vrq_scan.h"
+
+namespace vrq {
+
+constexpr int LOCAL_BITS = 20;
+constexpr uint32_t LOCAL_MASK = (1u << LOCAL_BITS) - 1;
+
+// Wave-level bitonic sort (ascending) of the CAP u32 keys at buf[0..CAP);
+// entries at index >= cnt are treated as +inf.  Result written back to buf.
+template <int CAP>
+__device__ __forceinline__ void wave_sort_keys(uint32_t* buf, int cnt) {
+  constexpr int E = CAP / WAVE;
+  const int l = lane_id();
+  uint32_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = e * WAVE + l;
+    v[e] = (i < cnt) ? buf[i] : 0xffffffffu;
+  }
+#pragma unroll
+  for (int size = 2; size <= CAP; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= WAVE) {
+        const int es = stride / WAVE;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if ((e & es) == 0) {
+            const int i = e * WAVE + l;
+            const bool up = (i & size) == 0;
+            const uint32_t a = v[e], b = v[e + es];
+            const uint32_t mn = a < b ? a : b, mx = a < b ? b : a;
+            v[e] = up ? mn : mx;
+            v[e + es] = up ? mx : mn;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = e * WAVE + l;
+          const uint32_t p = shfl_xor_u32(v[e], stride);
+          const bool up = (i & size) == 0;
+          const bool lower = (l & stride) == 0;
+          const uint32_t mn = v[e] < p ? v[e] : p, mx = v[e] < p ? p : v[e];
+          v[e] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) buf[e * WAVE + l] = v[e];
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
+}
+
+// 128 query bytes -> 32 SGPRs (two s_load_dwordx16 from the scalar cache) and the
+// wait, in ONE asm statement: the SGPRs are valid at ASMEND, so hipcc can neither
+// hoist the loads out of the tile loop (that spilled QG*32 SGPRs) nor copy or
+// spill the destinations before the data lands.
+__device__ __forceinline__ void load_q(v16u& a, v16u& b, const uint8_t* p) {
+  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(a), "=&s"(b)
+               : "s"(p)
+               : "memory");
+}
+
+// d += popcount(q ^ r): v_xor_b32 (SGPR q) + v_bcnt_u32_b32 (bcnt accumulates).  The
+// empty asm pins the accumulation order so LLVM does not re-associate the chain
+// into bcnt(x,0) + v_add3 trees (+15 % VALU).
+__device__ __forceinline__ void xor_bcnt(uint32_t& d, uint32_t q, uint32_t r) {
+  d = __popc(q ^ r) + d;
+  asm("" : "+v"(d));
+}
+
+template <int CB, int QG, int CAP, int NBUF>
+__global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restrict__ codes, int64_t n,
+                                                          const uint8_t* __restrict__ queries, int nq,
+                                                          int K, int64_t chunk_rows, int nchunks, int nqg,
+                                                          uint64_t* __restrict__ out) {
+  constexpr int C = CB / 16;          // 16-byte pieces per row
+  constexpr int TILE = 64 * CB;       // bytes per 64-row tile
+  constexpr int GLDS = TILE / 1024;   // LDS-DMA wave-instructions per tile
+  constexpr int RPG = 16 / C;         // rows per 16-slot bank period
+  static_assert(CB == 128, "scan kernel is specialised for 1024-bit codes");
+  static_assert(CAP % WAVE == 0, "cap");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NBUF * TILE + QG * CAP * 4];
+  uint32_t* cand = reinterpret_cast<uint32_t*>(smem + NBUF * TILE);
+
+  // XCD-aware, bijective block -> linear id (blocks b and b+8 share an XCD).
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3, q8 = nb >> 3, r8 = nb & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int chunk = L / nqg;
+  const int qg = L - chunk * nqg;
+  if (chunk >= nchunks) return;
+  const int64_t row0 = (int64_t)chunk * chunk_rows;
+  const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  const int nrows = (int)(row1 - row0);
+  const int l = lane_id();
+  const int nqa = (nq - qg * QG) < QG ? (nq - qg * QG) : QG;  // active queries in this group
+  const uint8_t* qbase = queries + (int64_t)qg * QG * CB;
+
+  int cnt[QG];
+  uint32_t tau[QG];
+#pragma unroll
+  for (int j = 0; j < QG; ++j) {
+    cnt[j] = 0;
+    tau[j] = 0xffffffffu;
+  }
+
+  // per-lane LDS addresses of this lane's row pieces (swizzled slots), tile 0
+  uint32_t raddr[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) raddr[c] = lds_addr(smem) + (uint32_t)((l * C + (c ^ ((l / RPG) % C))) * 16);
+
+  const int ntiles = (nrows + 63) >> 6;
+  auto issue = [&](int t) {
+    uint8_t* buf = smem + (t % NBUF) * TILE;
+    const int64_t tr0 = row0 + (int64_t)t * 64;
+#pragma unroll
+    for (int i = 0; i < GLDS; ++i) {
+      const int p = i * 64 + l;
+      const int r = p / C, cs = p % C;
+      const int c = cs ^ ((r / RPG) % C);
+      int64_t row = tr0 + r;
+      row = row < row1 ? row : row1 - 1;  // clamp the ragged last tile (lanes masked below)
+      __builtin_amdgcn_global_load_lds(codes + row * CB + c * 16,
+                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < NBUF; ++t)
+    if (t < ntiles) issue(t);
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + NBUF - 1 < ntiles)
+      wait_vmcnt<(NBUF - 1) * GLDS>();
+    else
+      wait_vmcnt<0>();
+    const uint32_t boff = (uint32_t)((t % NBUF) * TILE);
+    v4u rv[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(rv[c]) : "v"(raddr[c] + boff) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]), "+v"(rv[4]), "+v"(rv[5]), "+v"(rv[6]),
+                   "+v"(rv[7])::"memory");
+    if (t + NBUF < ntiles) issue(t + NBUF);  // buffer t%NBUF is free: the tile is in VGPRs
+
+    const int local = t * 64 + l;
+    const bool valid = local < nrows;
+#pragma unroll
+    for (int j = 0; j < QG; ++j) {
+      if (j >= nqa) break;
+      v16u x0, x1;
+      load_q(x0, x1, qbase + j * CB);
+      uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xor_bcnt(d0, x0[4 * c + 0], rv[c].x);
+        xor_bcnt(d1, x0[4 * c + 1], rv[c].y);
+        xor_bcnt(d0, x0[4 * c + 2], rv[c].z);
+        xor_bcnt(d1, x0[4 * c + 3], rv[c].w);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xor_bcnt(d0, x1[4 * c + 0], rv[4 + c].x);
+        xor_bcnt(d1, x1[4 * c + 1], rv[4 + c].y);
+        xor_bcnt(d0, x1[4 * c + 2], rv[4 + c].z);
+        xor_bcnt(d1, x1[4 * c + 3], rv[4 + c].w);
+      }
+      const uint32_t key = valid ? (((d0 + d1) << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu;
+      bool acc = key < tau[j];
+      uint64_t mask = __ballot(acc);
+      if (mask) {
+        int nnew = __popcll(mask);
+        uint32_t* cj = cand + j * CAP;
+        if (cnt[j] + nnew > CAP) {
+          wave_sort_keys<CAP>(cj, cnt[j]);
+          cnt[j] = cnt[j] < K ? cnt[j] : K;
+          if (cnt[j] >= K) tau[j] = __builtin_amdgcn_readfirstlane(cj[K - 1]);
+          acc = key < tau[j];
+          mask = __ballot(acc);
+          nnew = __popcll(mask);
+        }
+        if (acc) {
+          const int pos = cnt[j] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+          cj[pos] = key;
+        }
+        cnt[j] += nnew;
+      }
+    }
+  }
+
+  // chunk done: exact top-K per query -> global keys (dist << 40 | shard row), padded.
+#pragma unroll
+  for (int j = 0; j < QG; ++j) {
+    if (j >= nqa) break;
+    uint32_t* cj = cand + j * CAP;
+    wave_sort_keys<CAP>(cj, cnt[j]);
+    const int m = cnt[j] < K ? cnt[j] : K;
+    uint64_t* o = out + ((int64_t)(qg * QG + j) * nchunks + chunk) * K;
+    for (int i = l; i < K; i += WAVE) {
+      uint64_t gk = KEY_NONE;
+      if (i < m) {
+        const uint32_t key = cj[i];
+        gk = ((uint64_t)(key >> LOCAL_BITS) << KEY_ROW_BITS) | (uint64_t)(row0 + (key & LOCAL_MASK));
+      }
+      o[i] = gk;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side: plan + dispatch
+// ---------------------------------------------------------------------------
+static int cap_for(int K) {
+  int c = 128;
+  while (c < K + 64) c <<= 1;
+  return c;
+}
+
+int scan_plan(int64_t n, int cb, int nq, int K, ScanPlan* p) {
+  if (K < 1 || nq < 1 || n < 1) return VRQ_EINVAL;
+  if (cb != 128 || K > 1024) return VRQ_EUNSUPPORTED;
+  const int cap = cap_for(K);
+  int qgmax = 2048 / cap;
+  if (qgmax > 8) qgmax = 8;
+  int qg = 1;
+  while (qg < qgmax && qg < nq) qg <<= 1;
+  p->cap = cap;
+  p->qg = qg;
+  p->nqg = (nq + qg - 1) / qg;
+  int64_t want = kTargetWaves / p->nqg;
+  if (want < 1) want = 1;
+  int64_t cr = (n + want - 1) / want;
+  if (cr < kMinChunkRows) cr = kMinChunkRows;
+  cr = (cr + 63) & ~int64_t(63);
+  if (cr > (int64_t(1) << LOCAL_BITS)) cr = int64_t(1) << LOCAL_BITS;
+  // the merge (select_rescore.hip) takes at most 4096 lists per query
+  if ((n + cr - 1) / cr > 4096) cr = ((n + 4095) / 4096 + 63) & ~int64_t(63);
+  if (cr > (int64_t(1) << LOCAL_BITS)) return VRQ_EUNSUPPORTED;
+  p->chunk_rows = cr;
+  p->nchunks = (int)((n + cr - 1) / cr);
+  p->list_bytes = (size_t)nq * p->nchunks * K * sizeof(uint64_t);
+  return VRQ_OK;
+}
+
+template <int CB, int QG, int CAP>
+static int launch_t(const ScanPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
+                    uint64_t* lists, hipStream_t s) {
+  const int nblocks = p.nchunks * p.nqg;
+  hipLaunchKernelGGL((hamming_scan_kernel<CB, QG, CAP, 2>), dim3(nblocks), dim3(64), 0, s, codes, n, q, nq, K,
+                     p.chunk_rows, p.nchunks, p.nqg, lists);
+  VRQ_LAUNCH_CHECK();
+  return VRQ_OK;
+}
+
+int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, const uint8_t* q, int nq, int K,
+                uint64_t* lists, hipStream_t s) {
+  if (cb != 128) return VRQ_EUNSUPPORTED;
+  switch (p.cap) {
+    case 128:
+      switch (p.qg) {
+        case 1: return launch_t<128, 1, 128>(p, codes, n, q, nq, K, lists, s);
+        case 2: return launch_t<128, 2, 128>(p, codes, n, q, nq, K, lists, s);
+        case 4: return launch_t<128, 4, 128>(p, codes, n, q, nq, K, lists, s);
+        default: return launch_t<128, 8, 128>(p, codes, n, q, nq, K, lists, s);
+      }
+    case 256:
+      switch (p.qg) {
+        case 1: return launch_t<128, 1, 256>(p, codes, n, q, nq, K, lists, s);
+        case 2: return launch_t<128, 2, 256>(p, codes, n, q, nq, K, lists, s);
+        case 4: return launch_t<128, 4, 256>(p, codes, n, q, nq, K, lists, s);
+        default: return launch_t<128, 8, 256>(p, codes, n, q, nq, K, lists, s);
+      }
+    case 512:
+      switch (p.qg) {
+        case 1: return launch_t<128, 1, 512>(p, codes, n, q, nq, K, lists, s);
+        case 2: return launch_t<128, 2, 512>(p, codes, n, q, nq, K, lists, s);
+        default: return launch_t<128, 4, 512>(p, codes, n, q, nq, K, lists, s);
+      }
+    case 1024:
+      switch (p.qg) {
+        case 1: return launch_t<128, 1, 1024>(p, codes, n, q, nq, K, lists, s);
+        default: return launch_t<128, 2, 1024>(p, codes, n, q, nq, K, lists, s);
+      }
+    case 2048:
+      return launch_t<128, 1, 2048>(p, codes, n, q, nq, K, lists, s);
+    default:
+      return VRQ_EUNSUPPORTED;
+  }
+}
+
+}  // namespace vrq

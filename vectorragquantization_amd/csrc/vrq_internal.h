@@ -1,0 +1,112 @@
+// vrq_internal.h -- shared device helpers for the gfx950 kernels of libvrq.so.
+// Written for CDNA4 wave64 only (no CUDA/HIP dual paths).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vrq.h"
+
+namespace vrq {
+
+constexpr int WAVE = 64;
+constexpr uint64_t KEY_NONE = ~0ull;   // sentinel (dist = INF, row = max)
+constexpr int KEY_ROW_BITS = 40;       // global candidate key: dist << 40 | row
+constexpr int32_t DIST_NONE = 0x7fffffff;
+
+#define VRQ_CHECK_ARG(c)            \
+  do {                              \
+    if (!(c)) return VRQ_EINVAL;    \
+  } while (0)
+
+#define VRQ_LAUNCH_CHECK()                               \
+  do {                                                   \
+    if (hipPeekAtLastError() != hipSuccess) {            \
+      (void)hipGetLastError();                           \
+      return VRQ_EHIP;                                   \
+    }                                                    \
+  } while (0)
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {
+  return (uint32_t)__shfl_xor((int)v, m, WAVE);
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  uint32_t lo = shfl_xor_u32((uint32_t)v, m), hi = shfl_xor_u32((uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
+  return __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(v), m));
+}
+
+// f64 wave sum (butterfly; identical result in every lane)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) v += shfl_xor_f64(v, m);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) v += (int64_t)shfl_xor_u64((uint64_t)v, m);
+  return v;
+}
+
+// Sortable 64-bit image of a double for DESCENDING order: larger double -> smaller key.
+__device__ __forceinline__ uint64_t desc_key_f64(double x) {
+  uint64_t u = (uint64_t)__double_as_longlong(x);
+  u = (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);  // ascending image
+  return ~u;                                                            // descending
+}
+
+// Block-wide (LDS) bitonic sort of n_pow2 u64 keys, ascending.  All threads of the
+// block call it; n_pow2 is a power of two <= capacity of `a`.
+__device__ inline void block_bitonic_sort_u64(uint64_t* a, int n_pow2) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < (n_pow2 >> 1); i += blockDim.x) {
+        int lo = ((i / stride) * stride * 2) + (i % stride);
+        int hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        uint64_t x = a[lo], y = a[hi];
+        if ((x > y) == up) {
+          a[lo] = y;
+          a[hi] = x;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Same, sorting (key, payload) pairs by key.
+__device__ inline void block_bitonic_sort_kv(uint64_t* k, int32_t* v, int n_pow2) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < (n_pow2 >> 1); i += blockDim.x) {
+        int lo = ((i / stride) * stride * 2) + (i % stride);
+        int hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        uint64_t x = k[lo], y = k[hi];
+        if ((x > y) == up) {
+          k[lo] = y;
+          k[hi] = x;
+          int32_t t = v[lo];
+          v[lo] = v[hi];
+          v[hi] = t;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__host__ __device__ constexpr int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace vrq

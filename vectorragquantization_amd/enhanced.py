@@ -1,0 +1,279 @@
+"""``CohereEnhancedVectorDB`` on MI355X: the reference's three-phase search as
+gfx950 HIP kernels behind the same Python surface.
+
+Reference: ``CohereEnhancedVectorDB.py`` (aitrailblazer/VectorRAGQuantization).
+Same constructor (``:45-51``), ``add_documents`` (``:171-225``), ``search``
+(``:227-322``: same result dict keys and order), ``remove_document``
+(``:324-340``), ``save`` (``:342-347``), ``__len__`` (``:349``).  Additions for
+batch / benchmark use that bypass HTTP: ``add_vectors`` and ``search_vectors``.
+
+Storage (all HBM-resident, rows = FAISS internal indices): ubinary codes in a
+``BinaryIndexIDMap2`` (u8[n,128]), int8 vectors (int8[n,1024]; the RocksDict
+``"int8"`` values) and their float64 norms (computed once at add time by
+``vrq_int8_row_norms``); document texts stay on the host.  ``search_vectors``
+is ONE ``vrq_search3`` call for a whole query batch: Phase-I scan kernel + a
+merge/rescore kernel, no host round trip between phases.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+from dataclasses import dataclass
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .index import BinaryIndexIDMap2, _GrowBuffer, as_device_tensor
+from .quant import int8_row_norms
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class SearchBatch:
+    """Device-tensor result of ``search_vectors`` ([nq, k], rows padded with -1)."""
+    count: torch.Tensor      # i32[nq]
+    doc_id: torch.Tensor     # i64[nq, k] external ids
+    row: torch.Tensor        # i64[nq, k] internal rows
+    hamming: torch.Tensor    # i32[nq, k]
+    binary: torch.Tensor     # f64[nq, k]
+    cosine: torch.Tensor     # f64[nq, k]
+
+    def to_dicts(self, texts: dict | None = None) -> List[List[Dict]]:
+        cnt = self.count.cpu().numpy()
+        ids, ham = self.doc_id.cpu().numpy(), self.hamming.cpu().numpy()
+        b2, c3 = self.binary.cpu().numpy(), self.cosine.cpu().numpy()
+        out = []
+        for q in range(cnt.shape[0]):
+            res = []
+            for j in range(int(cnt[q])):
+                h = {"doc_id": int(ids[q, j]), "score_hamming": int(ham[q, j]),
+                     "score_binary": float(b2[q, j]), "score_cosine": float(c3[q, j])}
+                if texts is not None:
+                    h["doc"] = texts.get(int(ids[q, j]), "N/A")
+                res.append(h)
+            out.append(res)
+        return out
+
+
+def search3(codes: torch.Tensor, x8: torch.Tensor, norms: torch.Tensor, qf: torch.Tensor, qb: torch.Tensor,
+            k: int, K: int, K3: int, flags: int = 0, row_offset: int = 0, rescore_row: torch.Tensor | None = None,
+            workspace: torch.Tensor | None = None):
+    """Thin wrapper of ``vrq_search3``; returns (count, rows, dist, s2, s3) device tensors."""
+    dev = qf.device
+    nq = qf.shape[0]
+    n = codes.shape[0]
+    dim = qf.shape[1]
+    kout = K if flags & N.VRQ_SEARCH_SHARD else k
+    cnt = torch.empty((nq,), dtype=torch.int32, device=dev)
+    rows = torch.empty((nq, kout), dtype=torch.int64, device=dev)
+    dist = torch.empty((nq, kout), dtype=torch.int32, device=dev)
+    s2 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
+    s3 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
+    lib = N.load()
+    need = lib.vrq_search3_workspace_size(n, dim, nq, K) if n and nq and K else 0
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty((max(need, 8),), dtype=torch.uint8, device=dev)
+    rc = lib.vrq_search3(N.ptr(codes) if n else 0, N.ptr(x8) if n else 0, N.ptr(norms) if n else 0,
+                         N.ptr(rescore_row), n, dim, row_offset, N.ptr(qf), N.ptr(qb), nq, k, K, K3, flags,
+                         N.ptr(cnt), N.ptr(rows), N.ptr(dist), N.ptr(s2), N.ptr(s3), N.ptr(workspace),
+                         workspace.numel(), N.stream_handle(dev))
+    N.check(rc, "vrq_search3")
+    return cnt, rows, dist, s2, s3
+
+
+class CohereEnhancedVectorDB:
+    """Drop-in for the reference class (``CohereEnhancedVectorDB.py:30``)."""
+
+    def __init__(self, folder: str, model: str = "embed-english-v3.0", embedding_dim: int = 1024,
+                 index_type=None, index_args: List = None, rdict_options=None, *, provider=None,
+                 device=None):
+        if index_args is None:
+            index_args = [embedding_dim]
+        if provider is None:   # the reference reads COHERE_EMBED_ENDPOINT / _KEY and raises if unset (:67-75)
+            from .embed import CohereHTTPProvider
+            provider = CohereHTTPProvider(model=model)
+        self.provider = provider
+        self.embedding_dim = embedding_dim
+        self.model = model
+        self.folder = folder
+        self._setup_config(folder, model, embedding_dim)
+        path = os.path.join(folder, "index.bin")
+        if os.path.exists(path):
+            self.index = BinaryIndexIDMap2.read(path, device)
+            logger.info("Existing binary index loaded.")
+        else:
+            self.index = BinaryIndexIDMap2(index_args[0], device)
+        self.device = self.index.device
+        self._x8 = _GrowBuffer((embedding_dim,), torch.int8, self.device)
+        self._norms = _GrowBuffer((), torch.float64, self.device)
+        self.texts: Dict[int, str] = {}
+        self._load_docs()
+        self._ws = None
+
+    # -- config / persistence (reference :90-115, :342-347) -----------------------
+    def _setup_config(self, folder: str, model: str, embedding_dim: int):
+        config_path = os.path.join(folder, "config.json")
+        if not os.path.exists(config_path):
+            if os.path.exists(folder) and os.listdir(folder):
+                raise Exception(f"Folder {folder} contains files, but no config.json. "
+                                "To create a new database, the folder must be empty.")
+            os.makedirs(folder, exist_ok=True)
+            config = {"version": "1.0", "model": model, "embedding_dim": embedding_dim}
+            with open(config_path, "w") as f:
+                json.dump(config, f)
+        else:
+            with open(config_path) as f:
+                config = json.load(f)
+            if config.get("model") != model or config.get("embedding_dim") != embedding_dim:
+                logger.warning("Config model or embedding_dim mismatch. Overwriting config.")
+                config = {"version": "1.0", "model": model, "embedding_dim": embedding_dim}
+                with open(config_path, "w") as f:
+                    json.dump(config, f)
+        self.config = config
+
+    def _docs_path(self):
+        return os.path.join(self.folder, "docs")
+
+    def _load_docs(self):
+        p = self._docs_path()
+        if not os.path.exists(os.path.join(p, "int8.npy")):
+            return
+        x8 = np.load(os.path.join(p, "int8.npy"))
+        if x8.shape[0] != self.index.ntotal:
+            raise RuntimeError("docs/int8.npy does not match index.bin")
+        t = torch.from_numpy(x8).to(self.device)
+        self._x8.append(t)
+        self._norms.append(int8_row_norms(t))
+        with open(os.path.join(p, "texts.json")) as f:
+            self.texts = {int(a): b for a, b in json.load(f).items()}
+
+    def save(self):
+        """index.bin in FAISS's IBM2 format (:346) + the doc store (int8 rows, texts)."""
+        self.index.write(os.path.join(self.folder, "index.bin"))
+        p = self._docs_path()
+        os.makedirs(p, exist_ok=True)
+        np.save(os.path.join(p, "int8.npy"), self._x8.view().cpu().numpy())
+        with open(os.path.join(p, "texts.json"), "w") as f:
+            json.dump({str(a): b for a, b in self.texts.items()}, f)
+        logger.info("Binary index saved.")
+
+    def __len__(self):
+        return self.index.ntotal
+
+    # -- document management ---------------------------------------------------------
+    def __contains__(self, doc_id) -> bool:
+        return int(doc_id) in self.texts
+
+    def add_vectors(self, doc_ids, int8, ubinary, docs=None, save: bool = False) -> None:
+        """Append pre-computed (int8, ubinary) embeddings -- ``:217-221`` without HTTP."""
+        ids = np.asarray(doc_ids.cpu() if isinstance(doc_ids, torch.Tensor) else doc_ids, dtype=np.int64).reshape(-1)
+        x8 = as_device_tensor(int8, torch.int8, self.device).reshape(ids.shape[0], self.embedding_dim)
+        ub = as_device_tensor(ubinary, torch.uint8, self.device).reshape(ids.shape[0], self.embedding_dim // 8)
+        self.index.add_with_ids(ub, ids)
+        self._x8.append(x8)
+        self._norms.append(int8_row_norms(x8))
+        if docs is None:
+            docs = [""] * ids.shape[0]
+        for i, d in zip(ids.tolist(), docs):
+            self.texts[i] = d
+        if save:
+            self.save()
+
+    def add_documents(self, doc_ids: List[int], docs: List[str], batch_size: int = 64, save: bool = True):
+        if len(doc_ids) != len(docs):
+            raise ValueError("doc_ids and docs must have the same length.")
+        for doc_id in doc_ids:                                              # :190-192
+            if int(doc_id) in self.texts:
+                self.remove_document(doc_id, save=False)
+        for start in range(0, len(docs), batch_size):                      # :195-222
+            bi, bd = doc_ids[start:start + batch_size], docs[start:start + batch_size]
+            emb = self.provider.embed(bd, "search_document", ["int8", "ubinary"])
+            if not emb:
+                logger.error("Failed to retrieve embeddings for a batch.")
+                continue
+            try:
+                x8, ub = emb["int8"], emb["ubinary"]
+                if not isinstance(x8, torch.Tensor):
+                    x8 = np.array(x8, dtype=np.int8)
+                    ub = np.array(ub, dtype=np.uint8)
+            except Exception as e:
+                logger.error("Error processing embeddings: %s", str(e))
+                continue
+            self.add_vectors(bi, x8, ub, bd, save=False)
+        if save:
+            self.save()
+
+    def remove_document(self, doc_id: int, save: bool = True):
+        if int(doc_id) in self.texts:                                       # :333-336
+            keep = self.index.id_map != int(doc_id)
+            self.index._compact(keep)
+            self._x8.keep(keep)
+            self._norms.keep(keep)
+            del self.texts[int(doc_id)]
+            logger.info(f"Document {doc_id} removed.")
+        else:
+            logger.warning(f"Document {doc_id} not found in the database.")
+        if save:
+            self.save()
+
+    # -- search ------------------------------------------------------------------------
+    def search_vectors(self, qf, qb, k: int = 10, binary_oversample: int = 10,
+                       int8_oversample: int = 3) -> SearchBatch:
+        """Batched three-phase search of float32 [nq, d] / ubinary [nq, d/8] query embeddings."""
+        qf = as_device_tensor(qf, torch.float32, self.device).reshape(-1, self.embedding_dim)
+        qb = as_device_tensor(qb, torch.uint8, self.device).reshape(-1, self.embedding_dim // 8)
+        n = self.index.ntotal
+        if k < 0 or binary_oversample < 0 or int8_oversample < 0:
+            raise ValueError("k and oversample factors must be non-negative")
+        K = min(k * binary_oversample, n)                                   # :267
+        K3 = k * int8_oversample                                            # :297
+        if self._ws is None or self._ws.device != self.device:
+            self._ws = torch.empty((8,), dtype=torch.uint8, device=self.device)
+        lib = N.load()
+        need = lib.vrq_search3_workspace_size(n, self.embedding_dim, qf.shape[0], K) if n and K else 0
+        if self._ws.numel() < need:
+            self._ws = torch.empty((need,), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            cnt, rows, dist, s2, s3 = search3(self.index.codes, self._x8.view(), self._norms.view(), qf, qb,
+                                              k, K, K3, 0, 0, self.index.rescore_rows(), self._ws)
+        ids = torch.where(rows >= 0, self.index.id_map[rows.clamp_min(0)] if n else rows, rows)
+        return SearchBatch(cnt, ids, rows, dist, s2, s3)
+
+    def search(self, query: str, k: int = 10, binary_oversample: int = 10, int8_oversample: int = 3) -> List[Dict]:
+        if self.index.ntotal == 0:                                           # :247-249
+            logger.error("No documents indexed. Please add documents before searching.")
+            return []
+        emb = self.provider.embed([query], "search_query", ["float", "ubinary"])
+        if not emb:
+            logger.error("Query embedding generation failed.")
+            return []
+        try:
+            qf, qb = emb["float"], emb["ubinary"]
+        except Exception as e:
+            logger.error("Error processing query embeddings: %s", str(e))
+            return []
+        res = self.search_vectors(qf, qb, k, binary_oversample, int8_oversample)
+        return res.to_dicts(self.texts)[0]
+
+
+def find_closest_document(db: CohereEnhancedVectorDB, query: str) -> Dict:
+    """``CohereEnhancedVectorDB.py:355-360``."""
+    results = db.search(query, k=1)
+    return results[0] if results else {}
+
+
+def print_top_results(db: CohereEnhancedVectorDB, query: str, k: int = 10):
+    """``CohereEnhancedVectorDB.py:363-375``."""
+    results = db.search(query, k=k)
+    if results:
+        print(f"Top {k} Results:")
+        for res in results:
+            print(f"Doc ID: {res['doc_id']}, Cosine Score: {res['score_cosine']:.4f}")
+            print(f"Document: {res['doc']}")
+            print("-" * 40)
+    else:
+        print("No matching documents found.")
