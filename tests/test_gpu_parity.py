@@ -265,15 +265,16 @@ def test_rescore_entry_points(dev):
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = rng.standard_normal((3, 1024)).astype(np.float32) * 0.03
     cand = rng.integers(-1, n, (3, 20)).astype(np.int64)
-    x8_t = _t(x8, dev)
+    x8_t, qf_t, codes_t, cand_t = _t(x8, dev), _t(qf, dev), _t(codes, dev), _t(cand, dev)  # keep alive
     norms = int8_row_norms(x8_t)
     out2 = torch.empty((3, 20), dtype=torch.float64, device=dev)
     out3 = torch.empty((3, 20), dtype=torch.float64, device=dev)
     lib = N.load()
-    N.check(lib.vrq_rescore_binary(N.ptr(_t(qf, dev)), 3, 1024, N.ptr(_t(codes, dev)), n, N.ptr(_t(cand, dev)), 20,
-                                   N.ptr(out2), N.stream_handle(dev)), "rb")
-    N.check(lib.vrq_rescore_int8_cosine(N.ptr(_t(qf, dev)), 3, 1024, N.ptr(x8_t), N.ptr(norms), n,
-                                        N.ptr(_t(cand, dev)), 20, N.ptr(out3), N.stream_handle(dev)), "rc")
+    N.check(lib.vrq_rescore_binary(N.ptr(qf_t), 3, 1024, N.ptr(codes_t), n, N.ptr(cand_t), 20, N.ptr(out2),
+                                   N.stream_handle(dev)), "rb")
+    N.check(lib.vrq_rescore_int8_cosine(N.ptr(qf_t), 3, 1024, N.ptr(x8_t), N.ptr(norms), n, N.ptr(cand_t), 20,
+                                        N.ptr(out3), N.stream_handle(dev)), "rc")
+    torch.cuda.synchronize()
     o2, o3 = out2.cpu().numpy(), out3.cpu().numpy()
     for q in range(3):
         for j in range(20):

@@ -41,7 +41,10 @@ constexpr uint32_t LOCAL_MASK = (1u << LOCAL_BITS) - 1;
 template <int CAP>
 __device__ __forceinline__ void wave_sort_keys(uint32_t* buf, int cnt) {
   constexpr int E = CAP / WAVE;
-  const int l = lane_id();
+  int l = lane_id();
+  // opaque lane id: keeps the network's lane masks from being hoisted into the scan
+  // loop, where they would hold ~100 SGPRs live and push the resident query words out
+  asm volatile("" : "+v"(l));
   uint32_t v[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -114,21 +117,42 @@ __device__ __forceinline__ void xor_bcnt(uint32_t& d, uint32_t q, uint32_t r) {
   asm("" : "+v"(d));
 }
 
-template <int CB, int QG, int CAP, int NBUF>
-__global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restrict__ codes, int64_t n,
-                                                          const uint8_t* __restrict__ queries, int nq,
-                                                          int K, int64_t chunk_rows, int nchunks, int nqg,
-                                                          uint64_t* __restrict__ out) {
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {  // provably wave-uniform (SGPR) pointer
+  const uint64_t u = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// One workgroup = WPG waves scanning one CHUNK of rows for WPG*QG queries; every wave
+// owns QG queries (resident in SGPRs for the whole chunk) and the per-query top-K
+// state of those queries.  The 64-row tiles stream HBM -> LDS through a 3-deep
+// ring shared by the workgroup (each wave issues GLDS/WPG of the 8 LDS-DMA
+// instructions of a tile), so a row is fetched once per WPG*QG queries.
+template <int QG, int WPG, int CAP>
+__global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* __restrict__ codes, int64_t n,
+                                                                const uint8_t* __restrict__ queries, int nq,
+                                                                int K, int64_t chunk_rows, int nchunks, int nqg,
+                                                                uint64_t* __restrict__ out) {
+  constexpr int CB = 128;             // bytes per 1024-bit code
   constexpr int C = CB / 16;          // 16-byte pieces per row
   constexpr int TILE = 64 * CB;       // bytes per 64-row tile
-  constexpr int GLDS = TILE / 1024;   // LDS-DMA wave-instructions per tile
+  constexpr int GLDS = TILE / 1024;   // LDS-DMA wave-instructions per tile (8)
+  constexpr int GPW = GLDS / WPG;     // ... issued by each wave
   constexpr int RPG = 16 / C;         // rows per 16-slot bank period
-  static_assert(CB == 128, "scan kernel is specialised for 1024-bit codes");
+  constexpr int NBUF = 3;
+  static_assert(WPG >= 1 && WPG <= GLDS && (GLDS % WPG) == 0, "waves per group");
+  static_assert(QG == 1 || QG == 2, "queries per wave");
   static_assert(CAP % WAVE == 0, "cap");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[NBUF * TILE + QG * CAP * 4];
-  uint32_t* cand = reinterpret_cast<uint32_t*>(smem + NBUF * TILE);
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NBUF * TILE + WPG * QG * CAP * 4];
 
-  // XCD-aware, bijective block -> linear id (blocks b and b+8 share an XCD).
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* cand = reinterpret_cast<uint32_t*>(smem + NBUF * TILE) + wave * QG * CAP;
+
+  // XCD-aware, bijective block -> linear id (blocks b and b+8 share an XCD): blocks of
+  // one XCD take consecutive ids = the same chunk for successive query groups (L2 reuse).
   const int nb = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, slot = b >> 3, q8 = nb >> 3, r8 = nb & 7;
   const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
@@ -139,8 +163,14 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
   const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
   const int nrows = (int)(row1 - row0);
   const int l = lane_id();
-  const int nqa = (nq - qg * QG) < QG ? (nq - qg * QG) : QG;  // active queries in this group
-  const uint8_t* qbase = queries + (int64_t)qg * QG * CB;
+  const int qw0 = (qg * WPG + wave) * QG;                 // first query of this wave
+  const int nqa = nq - qw0 < QG ? (nq - qw0 > 0 ? nq - qw0 : 0) : QG;
+
+  // queries -> SGPRs once per chunk (32 SGPRs each)
+  v16u qa0, qa1, qb0, qb1;
+  const uint8_t* qptr = uniform_ptr(queries + (int64_t)(nqa > 0 ? qw0 : 0) * CB);
+  if (nqa > 0) load_q(qa0, qa1, qptr);
+  if (QG == 2 && nqa > 1) load_q(qb0, qb1, qptr + CB);
 
   int cnt[QG];
   uint32_t tau[QG];
@@ -150,8 +180,7 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
     tau[j] = 0xffffffffu;
   }
 
-  // per-lane LDS addresses of this lane's row pieces (swizzled slots), tile 0
-  uint32_t raddr[C];
+  uint32_t raddr[C];  // this lane's row pieces in buffer 0 (swizzled slots)
 #pragma unroll
   for (int c = 0; c < C; ++c) raddr[c] = lds_addr(smem) + (uint32_t)((l * C + (c ^ ((l / RPG) % C))) * 16);
 
@@ -160,25 +189,27 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
     uint8_t* buf = smem + (t % NBUF) * TILE;
     const int64_t tr0 = row0 + (int64_t)t * 64;
 #pragma unroll
-    for (int i = 0; i < GLDS; ++i) {
-      const int p = i * 64 + l;
+    for (int i = 0; i < GPW; ++i) {
+      const int gi = wave * GPW + i;
+      const int p = gi * 64 + l;
       const int r = p / C, cs = p % C;
       const int c = cs ^ ((r / RPG) % C);
       int64_t row = tr0 + r;
       row = row < row1 ? row : row1 - 1;  // clamp the ragged last tile (lanes masked below)
       __builtin_amdgcn_global_load_lds(codes + row * CB + c * 16,
-                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(buf + gi * 1024), 16, 0, 0);
     }
   };
-#pragma unroll
-  for (int t = 0; t < NBUF; ++t)
-    if (t < ntiles) issue(t);
+  issue(0);
+  if (ntiles > 1) issue(1);
 
   for (int t = 0; t < ntiles; ++t) {
-    if (t + NBUF - 1 < ntiles)
-      wait_vmcnt<(NBUF - 1) * GLDS>();
+    if (t + 1 < ntiles)
+      wait_vmcnt<GPW>();  // my pieces of tile t landed (tile t+1's still in flight)
     else
       wait_vmcnt<0>();
+    lds_barrier();        // everyone's pieces of t landed; everyone finished reading t-1
+    if (t + 2 < ntiles) issue(t + 2);  // into buffer (t+2)%3 == (t-1)%3
     const uint32_t boff = (uint32_t)((t % NBUF) * TILE);
     v4u rv[C];
 #pragma unroll
@@ -187,15 +218,14 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]), "+v"(rv[4]), "+v"(rv[5]), "+v"(rv[6]),
                    "+v"(rv[7])::"memory");
-    if (t + NBUF < ntiles) issue(t + NBUF);  // buffer t%NBUF is free: the tile is in VGPRs
 
     const int local = t * 64 + l;
     const bool valid = local < nrows;
 #pragma unroll
     for (int j = 0; j < QG; ++j) {
       if (j >= nqa) break;
-      v16u x0, x1;
-      load_q(x0, x1, qbase + j * CB);
+      const v16u& x0 = j ? qb0 : qa0;
+      const v16u& x1 = j ? qb1 : qa1;
       uint32_t d0 = 0, d1 = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -242,7 +272,7 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
     uint32_t* cj = cand + j * CAP;
     wave_sort_keys<CAP>(cj, cnt[j]);
     const int m = cnt[j] < K ? cnt[j] : K;
-    uint64_t* o = out + ((int64_t)(qg * QG + j) * nchunks + chunk) * K;
+    uint64_t* o = out + ((int64_t)(qw0 + j) * nchunks + chunk) * K;
     for (int i = l; i < K; i += WAVE) {
       uint64_t gk = KEY_NONE;
       if (i < m) {
@@ -258,7 +288,7 @@ __global__ __launch_bounds__(64) void hamming_scan_kernel(const uint8_t* __restr
 // host side: plan + dispatch
 // ---------------------------------------------------------------------------
 static int cap_for(int K) {
-  int c = 128;
+  int c = 256;
   while (c < K + 64) c <<= 1;
   return c;
 }
@@ -266,20 +296,19 @@ static int cap_for(int K) {
 int scan_plan(int64_t n, int cb, int nq, int K, ScanPlan* p) {
   if (K < 1 || nq < 1 || n < 1) return VRQ_EINVAL;
   if (cb != 128 || K > 1024) return VRQ_EUNSUPPORTED;
-  const int cap = cap_for(K);
-  int qgmax = 2048 / cap;
-  if (qgmax > 8) qgmax = 8;
-  int qg = 1;
-  while (qg < qgmax && qg < nq) qg <<= 1;
-  p->cap = cap;
-  p->qg = qg;
-  p->nqg = (nq + qg - 1) / qg;
-  int64_t want = kTargetWaves / p->nqg;
+  p->cap = cap_for(K);
+  p->qg = nq >= 2 ? 2 : 1;
+  const int waves_needed = (nq + p->qg - 1) / p->qg;
+  int wpg = 1;
+  while (wpg < 8 && wpg < waves_needed) wpg <<= 1;
+  p->wpg = wpg;
+  const int per_group = p->qg * wpg;
+  p->nqg = (nq + per_group - 1) / per_group;
+  int64_t want = kTargetWaves / ((int64_t)p->nqg * wpg);
   if (want < 1) want = 1;
   int64_t cr = (n + want - 1) / want;
   if (cr < kMinChunkRows) cr = kMinChunkRows;
   cr = (cr + 63) & ~int64_t(63);
-  if (cr > (int64_t(1) << LOCAL_BITS)) cr = int64_t(1) << LOCAL_BITS;
   // the merge (select_rescore.hip) takes at most 4096 lists per query
   if ((n + cr - 1) / cr > 4096) cr = ((n + 4095) / 4096 + 63) & ~int64_t(63);
   if (cr > (int64_t(1) << LOCAL_BITS)) return VRQ_EUNSUPPORTED;
@@ -289,49 +318,43 @@ int scan_plan(int64_t n, int cb, int nq, int K, ScanPlan* p) {
   return VRQ_OK;
 }
 
-template <int CB, int QG, int CAP>
+template <int QG, int WPG, int CAP>
 static int launch_t(const ScanPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
                     uint64_t* lists, hipStream_t s) {
   const int nblocks = p.nchunks * p.nqg;
-  hipLaunchKernelGGL((hamming_scan_kernel<CB, QG, CAP, 2>), dim3(nblocks), dim3(64), 0, s, codes, n, q, nq, K,
+  hipLaunchKernelGGL((hamming_scan_kernel<QG, WPG, CAP>), dim3(nblocks), dim3(64 * WPG), 0, s, codes, n, q, nq, K,
                      p.chunk_rows, p.nchunks, p.nqg, lists);
   VRQ_LAUNCH_CHECK();
   return VRQ_OK;
+}
+
+template <int QG, int CAP>
+static int launch_w(const ScanPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
+                    uint64_t* lists, hipStream_t s) {
+  switch (p.wpg) {
+    case 1: return launch_t<QG, 1, CAP>(p, codes, n, q, nq, K, lists, s);
+    case 2: return launch_t<QG, 2, CAP>(p, codes, n, q, nq, K, lists, s);
+    case 4: return launch_t<QG, 4, CAP>(p, codes, n, q, nq, K, lists, s);
+    default: return launch_t<QG, 8, CAP>(p, codes, n, q, nq, K, lists, s);
+  }
+}
+
+template <int CAP>
+static int launch_c(const ScanPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
+                    uint64_t* lists, hipStream_t s) {
+  return p.qg == 1 ? launch_w<1, CAP>(p, codes, n, q, nq, K, lists, s)
+                   : launch_w<2, CAP>(p, codes, n, q, nq, K, lists, s);
 }
 
 int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, const uint8_t* q, int nq, int K,
                 uint64_t* lists, hipStream_t s) {
   if (cb != 128) return VRQ_EUNSUPPORTED;
   switch (p.cap) {
-    case 128:
-      switch (p.qg) {
-        case 1: return launch_t<128, 1, 128>(p, codes, n, q, nq, K, lists, s);
-        case 2: return launch_t<128, 2, 128>(p, codes, n, q, nq, K, lists, s);
-        case 4: return launch_t<128, 4, 128>(p, codes, n, q, nq, K, lists, s);
-        default: return launch_t<128, 8, 128>(p, codes, n, q, nq, K, lists, s);
-      }
-    case 256:
-      switch (p.qg) {
-        case 1: return launch_t<128, 1, 256>(p, codes, n, q, nq, K, lists, s);
-        case 2: return launch_t<128, 2, 256>(p, codes, n, q, nq, K, lists, s);
-        case 4: return launch_t<128, 4, 256>(p, codes, n, q, nq, K, lists, s);
-        default: return launch_t<128, 8, 256>(p, codes, n, q, nq, K, lists, s);
-      }
-    case 512:
-      switch (p.qg) {
-        case 1: return launch_t<128, 1, 512>(p, codes, n, q, nq, K, lists, s);
-        case 2: return launch_t<128, 2, 512>(p, codes, n, q, nq, K, lists, s);
-        default: return launch_t<128, 4, 512>(p, codes, n, q, nq, K, lists, s);
-      }
-    case 1024:
-      switch (p.qg) {
-        case 1: return launch_t<128, 1, 1024>(p, codes, n, q, nq, K, lists, s);
-        default: return launch_t<128, 2, 1024>(p, codes, n, q, nq, K, lists, s);
-      }
-    case 2048:
-      return launch_t<128, 1, 2048>(p, codes, n, q, nq, K, lists, s);
-    default:
-      return VRQ_EUNSUPPORTED;
+    case 256: return launch_c<256>(p, codes, n, q, nq, K, lists, s);
+    case 512: return launch_c<512>(p, codes, n, q, nq, K, lists, s);
+    case 1024: return launch_c<1024>(p, codes, n, q, nq, K, lists, s);
+    case 2048: return launch_c<2048>(p, codes, n, q, nq, K, lists, s);
+    default: return VRQ_EUNSUPPORTED;
   }
 }
 

@@ -16,7 +16,8 @@ constexpr int64_t kMinChunkRows = 4096;
 
 struct ScanPlan {
   int cap;             // per-query LDS candidate capacity (pow2 >= K + 64)
-  int qg;              // queries per wave
+  int qg;              // queries per wave (resident in SGPRs)
+  int wpg;             // waves per workgroup (share one LDS tile ring)
   int nqg;             // query groups
   int64_t chunk_rows;  // rows per wave (multiple of 64, <= 2^20)
   int nchunks;

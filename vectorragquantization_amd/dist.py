@@ -79,10 +79,10 @@ def merge_shards(cnt, rows, d, s2, s3, k: int, K3: int):
     o2 = torch.empty((nq, k), dtype=torch.float64, device=dev)
     o3 = torch.empty((nq, k), dtype=torch.float64, device=dev)
     src = torch.empty((nq, k), dtype=torch.int32, device=dev)
+    cnt, rows, d, s2, s3 = (t.contiguous() for t in (cnt, rows, d, s2, s3))  # held until the launch returns
     lib = N.load()
     with torch.cuda.device(dev):
-        rc = lib.vrq_merge_shards(S, nq, K, N.ptr(cnt.contiguous()), N.ptr(rows.contiguous()),
-                                  N.ptr(d.contiguous()), N.ptr(s2.contiguous()), N.ptr(s3.contiguous()), k, K3,
+        rc = lib.vrq_merge_shards(S, nq, K, N.ptr(cnt), N.ptr(rows), N.ptr(d), N.ptr(s2), N.ptr(s3), k, K3,
                                   N.ptr(oc), N.ptr(orow), N.ptr(od), N.ptr(o2), N.ptr(o3), N.ptr(src),
                                   N.stream_handle(dev))
     N.check(rc, "vrq_merge_shards")

@@ -67,7 +67,7 @@ def search3(codes: torch.Tensor, x8: torch.Tensor, norms: torch.Tensor, qf: torc
     nq = qf.shape[0]
     n = codes.shape[0]
     dim = qf.shape[1]
-    kout = K if flags & N.VRQ_SEARCH_SHARD else k
+    kout = K if flags & (N.VRQ_SEARCH_SHARD | N.VRQ_SEARCH_PHASE1_ONLY) else k
     cnt = torch.empty((nq,), dtype=torch.int32, device=dev)
     rows = torch.empty((nq, kout), dtype=torch.int64, device=dev)
     dist = torch.empty((nq, kout), dtype=torch.int32, device=dev)
