@@ -42,7 +42,10 @@ from vectorragquantization_amd.dist import gather_candidates, merge_shards, pack
 
 METRIC = "queries/sec + recall@10 vs float32, d=1024 3-phase search at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0                          # MI355X spec (MI355X_MICROARCH.md)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+# integer VALU peak: a wave64 v_xor_b32 / v_bcnt_u32_b32 retires every 4 SIMD cycles when the SIMD is
+# saturated (measured: tools/probes/valu_probe.hip, profiles/r1_valu_probe.json) ->
+# 1024 SIMDs x 64 lanes / 4 cycles x 2.4 GHz = 39.3 T lane-ops/s
+VALU_PEAK_TOPS = 1024 * 64 / 4 * 2.4e9 / 1e12
 
 
 def parse():

@@ -1,0 +1,57 @@
+#!/usr/bin/env python
+"""Condense rocprofv3 outputs (kernel-trace stats CSV + separate --pmc passes) into the JSON
+summaries committed under profiles/ (per round), incl. per-launch HBM traffic of the scan
+kernel corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE reads 1/2 of the bytes
+of 16-B-per-lane streams -> x2; WRITE_SIZE exact for 16-B stores; both in KiB)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    if "hamming_scan" in name:
+        return "hamming_scan_kernel"
+    if "select_rescore" in name:
+        return "select_rescore_kernel"
+    if "merge_shards" in name:
+        return "merge_shards_kernel"
+    if "encode_kernel" in name:
+        return "encode_kernel"
+    return name[:60]
+
+
+def pmc(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} | {"dispatches": len(next(iter(d.values())))}
+            for k, d in agg.items()}
+
+
+def main(src, dst, tag):
+    out = {"tag": tag, "source": src}
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if stats:
+        out["kernel_stats"] = [r for r in csv.DictReader(open(stats[0]))]
+    for name in ("pmc_sq", "pmc_fetch", "pmc_write"):
+        f = glob.glob(os.path.join(src, name, "*counter_collection.csv"))
+        if f:
+            out[name] = pmc(f[0])
+    scan = "hamming_scan_kernel"
+    try:
+        fetch = out["pmc_fetch"][scan]["FETCH_SIZE"] * 1024 * 2
+        write = out["pmc_write"][scan]["WRITE_SIZE"] * 1024
+        out["scan_bytes_per_launch"] = fetch + write
+        out["scan_fetch_bytes_corrected"] = fetch
+        out["scan_write_bytes"] = write
+    except KeyError:
+        pass
+    json.dump(out, open(dst, "w"), indent=1)
+    print("wrote", dst)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3])

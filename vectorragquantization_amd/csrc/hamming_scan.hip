@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* _
   constexpr int GLDS = TILE / 1024;   // LDS-DMA wave-instructions per tile (8)
   constexpr int GPW = GLDS / WPG;     // ... issued by each wave
   constexpr int RPG = 16 / C;         // rows per 16-slot bank period
-  constexpr int NBUF = 3;
+  constexpr int NBUF = 4;
   static_assert(WPG >= 1 && WPG <= GLDS && (GLDS % WPG) == 0, "waves per group");
   static_assert(QG == 1 || QG == 2, "queries per wave");
   static_assert(CAP % WAVE == 0, "cap");
@@ -200,69 +200,117 @@ __global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* _
                                        (__attribute__((address_space(3))) void*)(buf + gi * 1024), 16, 0, 0);
     }
   };
-  issue(0);
-  if (ntiles > 1) issue(1);
-
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles)
-      wait_vmcnt<GPW>();  // my pieces of tile t landed (tile t+1's still in flight)
-    else
-      wait_vmcnt<0>();
-    lds_barrier();        // everyone's pieces of t landed; everyone finished reading t-1
-    if (t + 2 < ntiles) issue(t + 2);  // into buffer (t+2)%3 == (t-1)%3
+  auto read_tile = [&](int t, v4u (&rv)[C]) {
     const uint32_t boff = (uint32_t)((t % NBUF) * TILE);
-    v4u rv[C];
 #pragma unroll
     for (int c = 0; c < C; ++c)
       asm volatile("ds_read_b128 %0, %1" : "=v"(rv[c]) : "v"(raddr[c] + boff) : "memory");
+  };
+  auto wait_tile = [&](v4u (&rv)[C]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]), "+v"(rv[4]), "+v"(rv[5]), "+v"(rv[6]),
                    "+v"(rv[7])::"memory");
-
-    const int local = t * 64 + l;
-    const bool valid = local < nrows;
+  };
+  // Distances of this lane's row to the wave's (up to) two queries; the two queries'
+  // four popcount chains are interleaved for ILP.
+  auto distances = [&](const v4u (&rv)[C], uint32_t& da, uint32_t& db) {
+    uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
 #pragma unroll
-    for (int j = 0; j < QG; ++j) {
-      if (j >= nqa) break;
-      const v16u& x0 = j ? qb0 : qa0;
-      const v16u& x1 = j ? qb1 : qa1;
-      uint32_t d0 = 0, d1 = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        xor_bcnt(d0, x0[4 * c + 0], rv[c].x);
-        xor_bcnt(d1, x0[4 * c + 1], rv[c].y);
-        xor_bcnt(d0, x0[4 * c + 2], rv[c].z);
-        xor_bcnt(d1, x0[4 * c + 3], rv[c].w);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        xor_bcnt(d0, x1[4 * c + 0], rv[4 + c].x);
-        xor_bcnt(d1, x1[4 * c + 1], rv[4 + c].y);
-        xor_bcnt(d0, x1[4 * c + 2], rv[4 + c].z);
-        xor_bcnt(d1, x1[4 * c + 3], rv[4 + c].w);
-      }
-      const uint32_t key = valid ? (((d0 + d1) << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu;
-      bool acc = key < tau[j];
-      uint64_t mask = __ballot(acc);
-      if (mask) {
-        int nnew = __popcll(mask);
-        uint32_t* cj = cand + j * CAP;
-        if (cnt[j] + nnew > CAP) {
-          wave_sort_keys<CAP>(cj, cnt[j]);
-          cnt[j] = cnt[j] < K ? cnt[j] : K;
-          if (cnt[j] >= K) tau[j] = __builtin_amdgcn_readfirstlane(cj[K - 1]);
-          acc = key < tau[j];
-          mask = __ballot(acc);
-          nnew = __popcll(mask);
-        }
-        if (acc) {
-          const int pos = cnt[j] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-          cj[pos] = key;
-        }
-        cnt[j] += nnew;
-      }
+    for (int c = 0; c < 4; ++c) {
+      xor_bcnt(a0, qa0[4 * c + 0], rv[c].x);
+      if (QG == 2) xor_bcnt(b0, qb0[4 * c + 0], rv[c].x);
+      xor_bcnt(a1, qa0[4 * c + 1], rv[c].y);
+      if (QG == 2) xor_bcnt(b1, qb0[4 * c + 1], rv[c].y);
+      xor_bcnt(a0, qa0[4 * c + 2], rv[c].z);
+      if (QG == 2) xor_bcnt(b0, qb0[4 * c + 2], rv[c].z);
+      xor_bcnt(a1, qa0[4 * c + 3], rv[c].w);
+      if (QG == 2) xor_bcnt(b1, qb0[4 * c + 3], rv[c].w);
     }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      xor_bcnt(a0, qa1[4 * c + 0], rv[4 + c].x);
+      if (QG == 2) xor_bcnt(b0, qb1[4 * c + 0], rv[4 + c].x);
+      xor_bcnt(a1, qa1[4 * c + 1], rv[4 + c].y);
+      if (QG == 2) xor_bcnt(b1, qb1[4 * c + 1], rv[4 + c].y);
+      xor_bcnt(a0, qa1[4 * c + 2], rv[4 + c].z);
+      if (QG == 2) xor_bcnt(b0, qb1[4 * c + 2], rv[4 + c].z);
+      xor_bcnt(a1, qa1[4 * c + 3], rv[4 + c].w);
+      if (QG == 2) xor_bcnt(b1, qb1[4 * c + 3], rv[4 + c].w);
+    }
+    da = a0 + a1;
+    db = b0 + b1;
+  };
+  auto accept = [&](int j, uint32_t key) {
+    bool acc = key < tau[j];
+    uint64_t mask = __ballot(acc);
+    if (mask) {
+      int nnew = __popcll(mask);
+      uint32_t* cj = cand + j * CAP;
+      if (cnt[j] + nnew > CAP) {
+        wave_sort_keys<CAP>(cj, cnt[j]);
+        cnt[j] = cnt[j] < K ? cnt[j] : K;
+        if (cnt[j] >= K) tau[j] = __builtin_amdgcn_readfirstlane(cj[K - 1]);
+        acc = key < tau[j];
+        mask = __ballot(acc);
+        nnew = __popcll(mask);
+      }
+      if (acc) {
+        const int pos = cnt[j] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        cj[pos] = key;
+      }
+      cnt[j] += nnew;
+    }
+  };
+
+  // Software pipeline over a 4-deep LDS ring: while tile t is computed from VGPRs
+  // (set A), tile t+1 is read LDS -> VGPRs (set B) and tiles t+2, t+3 are in flight
+  // HBM -> LDS.  One workgroup barrier per tile publishes tile t+1 (every wave's DMA
+  // pieces waited by that wave's vmcnt) and certifies that every wave finished
+  // reading tile t-1, whose buffer (t+3)%4 is then refilled.
+  for (int t = 0; t < 3 && t < ntiles; ++t) issue(t);
+  if (ntiles > 2)
+    wait_vmcnt<2 * GPW>();
+  else if (ntiles > 1)
+    wait_vmcnt<GPW>();
+  else
+    wait_vmcnt<0>();
+  lds_barrier();
+  v4u rA[C], rB[C];
+  read_tile(0, rA);
+  wait_tile(rA);
+  for (int t = 0; t < ntiles; t += 2) {
+    // ---- tile t from A, prefetch t+1 into B
+    if (t + 1 < ntiles) {
+      if (t + 2 < ntiles) wait_vmcnt<GPW>(); else wait_vmcnt<0>();
+      lds_barrier();
+      read_tile(t + 1, rB);
+      if (t + 3 < ntiles) issue(t + 3);
+    }
+    {
+      const int local = t * 64 + l;
+      uint32_t da, db;
+      distances(rA, da, db);
+      if (nqa > 0) accept(0, local < nrows ? ((da << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
+      if (QG == 2 && nqa > 1) accept(1, local < nrows ? ((db << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
+    }
+    if (t + 1 >= ntiles) break;
+    wait_tile(rB);
+    // ---- tile t+1 from B, prefetch t+2 into A
+    if (t + 2 < ntiles) {
+      if (t + 3 < ntiles) wait_vmcnt<GPW>(); else wait_vmcnt<0>();
+      lds_barrier();
+      read_tile(t + 2, rA);
+      if (t + 4 < ntiles) issue(t + 4);
+    }
+    {
+      const int local = (t + 1) * 64 + l;
+      uint32_t da, db;
+      distances(rB, da, db);
+      if (nqa > 0) accept(0, local < nrows ? ((da << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
+      if (QG == 2 && nqa > 1) accept(1, local < nrows ? ((db << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
+    }
+    if (t + 2 < ntiles) wait_tile(rA);
   }
 
   // chunk done: exact top-K per query -> global keys (dist << 40 | shard row), padded.
