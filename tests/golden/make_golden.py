@@ -363,7 +363,9 @@ def gen_search_real(out_path: str):
     QB = np.stack([O.to_binary_sign(x) for x in QF])
     res = {"codes": xb, "int8": I8, "qsrc": qsrc, "qf": QF, "qb": QB,
            "gt_float_top10": O.float_ip_topk(F, QF, 10),
-           "sign_bits_mismatch": np.int64((np.stack([O.to_binary_sign(x) for x in F]) != xb).sum())}
+           "sign_bits_mismatch": np.int64((np.stack([O.to_binary_sign(x) for x in F]) != xb).sum()),
+           "index_bin_sha256": np.frombuffer(__import__("hashlib").sha256(
+               open(os.path.join(REF, "db_cohere_enhanced/index.bin"), "rb").read()).digest(), np.uint8)}
     r = search_table(db, QF, QB, 10, 10, 3, qlk)
     for kk, v in r.items():
         res[f"k10_{kk}"] = v

@@ -1,0 +1,139 @@
+"""Multi-rank path on CPU (gloo, world_size 2): shard plan, candidate packing, the single
+all-gather collective, and -- with the CPU oracle standing in for the per-shard kernels
+(test infrastructure) -- that the merged result equals the single-index reference.  The
+GPU merge kernel itself (vrq_merge_shards) is checked against the single-GPU search in
+tests/test_gpu_parity.py::test_shard_mode_and_merge_equal_single_index."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle_np as O
+from vectorragquantization_amd import synth
+from vectorragquantization_amd.dist import gather_candidates, pack_candidates, unpack_candidates
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _corpus():
+    rng = np.random.default_rng(123)
+    n, nq = 4000, 12
+    F = rng.standard_normal((n, 1024)).astype(np.float32) * 0.03
+    F[2100:2200] = F[0:100]                                  # duplicates across the two shards
+    codes, x8, _ = O.encode_batch("cohere", F, 0.1)
+    qf = (F[rng.integers(0, n, nq)] + 0.01 * rng.standard_normal((nq, 1024))).astype(np.float32)
+    qb, _, _ = O.encode_batch("cohere", qf, 0.1)
+    return codes, x8, qf, qb
+
+
+def _shard_candidates(codes, x8, qf, qb, r0, r1, K):
+    """Oracle stand-in for vrq_search3(..., VRQ_SEARCH_SHARD): this shard's exact top-K by
+    (dist, global row) with Phase-II / Phase-III scores."""
+    nq = qf.shape[0]
+    cnt = np.zeros(nq, np.int32)
+    rows = np.full((nq, K), -1, np.int64)
+    d = np.full((nq, K), np.iinfo(np.int32).max, np.int32)
+    s2 = np.full((nq, K), np.nan)
+    s3 = np.full((nq, K), np.nan)
+    D, I = O.binary_flat_search(codes[r0:r1], qb, K)
+    norms = O.int8_row_norms(x8)
+    for q in range(nq):
+        m = int((I[q] >= 0).sum())
+        cnt[q] = m
+        for j in range(m):
+            r = int(I[q, j]) + r0
+            rows[q, j], d[q, j] = r, D[q, j]
+            s2[q, j] = float(qf[q].dot(2 * np.unpackbits(codes[r]).astype(np.int32) - 1))
+            s3[q, j] = -np.inf if norms[r] == 0 else float(qf[q].dot(x8[r])) / norms[r]
+    return cnt, rows, d, s2, s3
+
+
+def _merge_oracle(gc, gr, gd, g2, g3, k, K3):
+    """Host restatement of vrq_merge_shards: top-K by (dist, row) -> stable s2 -> K3 -> stable s3 -> k."""
+    S, nq, K = gr.shape
+    out = []
+    for q in range(nq):
+        c = [(int(gd[s, q, p]), int(gr[s, q, p]), g2[s, q, p], g3[s, q, p])
+             for s in range(S) for p in range(int(gc[s, q]))]
+        c.sort(key=lambda t: (t[0], t[1]))
+        c = c[:K]
+        c = sorted(c, key=lambda t: -t[2])[:K3]
+        c = sorted(c, key=lambda t: -t[3])[:k]
+        out.append([t[1] for t in c])
+    return out
+
+
+def _worker(rank, world, port, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    codes, x8, qf, qb = _corpus()
+    n, k, osb, osi = codes.shape[0], 10, 10, 3
+    K = min(k * osb, n)
+    r0, r1 = synth.shard_range(n, rank, world)
+    cnt, rows, d, s2, s3 = _shard_candidates(codes, x8, qf, qb, r0, r1, K)
+    ids = np.where(rows >= 0, rows + 7, -1)                       # external id = row + 7
+    t = [torch.from_numpy(a) for a in (cnt, rows, ids, d, s2, s3)]
+    buf = gather_candidates(pack_candidates(*t))                   # one collective
+    gc, gr, gi, gd, g2, g3 = (x.numpy() for x in unpack_candidates(buf, world, qf.shape[0], K))
+    merged = _merge_oracle(gc, gr, gd, g2, g3, k, k * osi)
+    if rank == 0:
+        ref = O.three_phase_batch(codes, x8, np.arange(n) + 7, qf, qb, k, osb, osi)
+        ok = all(merged[q] == ref[q]["row"].tolist() for q in range(qf.shape[0]))
+        # ids travel with their rows through the gather
+        ok &= bool(np.all((gi[gr >= 0] == gr[gr >= 0] + 7)))
+        result_q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_ranges_cover_and_align():
+    for n in (1, 63, 64, 1000, 1_000_000, 100_000_000):
+        for world in (1, 2, 4, 8):
+            rs = [synth.shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            cs = synth.chunk_grid(n)
+            assert all(a % cs == 0 or a == n for a, _ in rs)
+
+
+def test_pack_unpack_roundtrip():
+    nq, K, S = 5, 7, 3
+    parts = []
+    for s in range(S):
+        g = torch.Generator().manual_seed(s)
+        parts.append((torch.randint(0, K, (nq,), dtype=torch.int32, generator=g),
+                      torch.randint(0, 1 << 40, (nq, K), generator=g),
+                      torch.randint(0, 1 << 40, (nq, K), generator=g),
+                      torch.randint(0, 1025, (nq, K), dtype=torch.int32, generator=g),
+                      torch.randn((nq, K), dtype=torch.float64, generator=g),
+                      torch.randn((nq, K), dtype=torch.float64, generator=g)))
+    buf = torch.cat([pack_candidates(*p) for p in parts])
+    out = unpack_candidates(buf, S, nq, K)
+    for s in range(S):
+        c, r, i, d, a, b = parts[s]
+        assert torch.equal(out[0][s], c) and torch.equal(out[1][s], r) and torch.equal(out[2][s], i)
+        assert torch.equal(out[3][s], d) and torch.equal(out[4][s], a) and torch.equal(out[5][s], b)
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_sharded_search_equals_single_index():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True

@@ -45,6 +45,29 @@ def torch_to_np(dtype):
             torch.int64: np.int64, torch.float32: np.float32, torch.float64: np.float64}[dtype]
 
 
+def ibm2_pack(d: int, codes: np.ndarray, ids: np.ndarray) -> bytes:
+    """FAISS ``write_index_binary`` image of ``IndexBinaryIDMap2(IndexBinaryFlat(d))``:
+    "IBM2" + header(d, code_size, ntotal, is_trained, metric) + "IBxF" + header + xb + id_map."""
+    n = int(codes.shape[0])
+    hdr = struct.pack("<iiqbi", d, d // 8, n, 1, 1)
+    xb = np.ascontiguousarray(codes, dtype=np.uint8).tobytes()
+    return (b"IBM2" + hdr + b"IBxF" + hdr + struct.pack("<q", len(xb)) + xb + struct.pack("<q", n)
+            + np.ascontiguousarray(ids, dtype="<i8").tobytes())
+
+
+def ibm2_unpack(b: bytes):
+    """Inverse of ``ibm2_pack`` -> (d, codes u8[n, d/8], ids i64[n])."""
+    if b[:4] != b"IBM2" or b[25:29] != b"IBxF":
+        raise ValueError("not a FAISS IndexBinaryIDMap2(IndexBinaryFlat) file")
+    d, cs, nt, _, _ = struct.unpack("<iiqbi", b[4:25])
+    off = 50
+    nb, = struct.unpack("<q", b[off:off + 8]); off += 8
+    xb = np.frombuffer(b, np.uint8, nb, off).reshape(nt, cs); off += nb
+    ni, = struct.unpack("<q", b[off:off + 8]); off += 8
+    ids = np.frombuffer(b, "<i8", ni, off)
+    return d, xb, ids
+
+
 class _GrowBuffer:
     """Row-major device buffer with geometric capacity growth."""
 
@@ -182,12 +205,7 @@ class BinaryIndexIDMap2:
 
     # -- FAISS IBM2 on-disk format (faiss.write_index_binary / read_index_binary) ----
     def to_bytes(self) -> bytes:
-        n = self.ntotal
-        hdr = struct.pack("<iiqbi", self.d, self.code_size, n, 1, 1)
-        xb = self.codes.cpu().numpy().tobytes()
-        ids = self.id_map.cpu().numpy().astype("<i8").tobytes()
-        return (b"IBM2" + hdr + b"IBxF" + hdr + struct.pack("<q", len(xb)) + xb
-                + struct.pack("<q", n) + ids)
+        return ibm2_pack(self.d, self.codes.cpu().numpy(), self.id_map.cpu().numpy())
 
     def write(self, path: str) -> None:
         with open(path, "wb") as f:
@@ -195,16 +213,9 @@ class BinaryIndexIDMap2:
 
     @classmethod
     def from_bytes(cls, b: bytes, device=None) -> "BinaryIndexIDMap2":
-        if b[:4] != b"IBM2" or b[25:29] != b"IBxF":
-            raise ValueError("not a FAISS IndexBinaryIDMap2(IndexBinaryFlat) file")
-        d, cs, nt, _, _ = struct.unpack("<iiqbi", b[4:25])
-        off = 50
-        nb, = struct.unpack("<q", b[off:off + 8]); off += 8
-        xb = np.frombuffer(b, np.uint8, nb, off).reshape(nt, cs); off += nb
-        ni, = struct.unpack("<q", b[off:off + 8]); off += 8
-        ids = np.frombuffer(b, "<i8", ni, off)
+        d, xb, ids = ibm2_unpack(b)
         idx = cls(d, device)
-        if nt:
+        if xb.shape[0]:
             idx.add_with_ids(xb, ids)
         return idx
 
