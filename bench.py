@@ -104,7 +104,7 @@ class Pipeline:
         if record:
             e[0].record()
         N.check(L.vrq_search3_scan(N.ptr(self.codes), self.m, 1024, N.ptr(self.qb), self.qb.shape[0], self.K,
-                                   N.ptr(self.ws), self.ws.numel(), st), "scan")
+                                   self.flags, N.ptr(self.ws), self.ws.numel(), st), "scan")
         if record:
             e[1].record()
         N.check(L.vrq_search3_finish(N.ptr(self.codes), N.ptr(self.x8), N.ptr(self.norms), None, self.m, 1024,

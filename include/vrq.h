@@ -45,6 +45,16 @@ extern "C" {
                                     (dist,row) order with Phase-II AND Phase-III
                                     scores, no Phase II/III sort (merged later by
                                     vrq_merge_shards) */
+#define VRQ_SEARCH_SCAN_VALU 4   /* Phase-I scan: force the wavefront popcount scan */
+#define VRQ_SEARCH_SCAN_MFMA 8   /* Phase-I scan: force the matrix-core scan wherever it is
+                                    supported (K <= 128, n >= 65536); by default it is used for
+                                    nq >= 128.  Both scans give identical results. */
+/* vrq_search3_scan only, matrix-core scan only: run a subset of its three stages (none set =
+ * all), so a caller can bracket each stage with events; issuing the three in order on one
+ * stream is exactly the full scan. */
+#define VRQ_SCAN_STAGE_PREFIX 16 /* exact scan of the prefix rows -> per-query threshold */
+#define VRQ_SCAN_STAGE_MATRIX 32 /* hamming_mfma_kernel over the suffix rows */
+#define VRQ_SCAN_STAGE_SUFFIX 64 /* suffix candidates -> one sorted list (exact rescan on overflow) */
 
 /* encoder modes for vrq_encode */
 #define VRQ_ENC_INT8_GLOBAL 0  /* VectorDBInt8Global._quantize_to_int8 + _to_binary */
@@ -102,9 +112,10 @@ int vrq_search3(const uint8_t* codes, const int8_t* x8, const double* norms, con
 /* The two launches vrq_search3 is made of, for callers that time or overlap them:
  * vrq_search3_scan   -- K1, the Phase-I scan: per-chunk exact top-K lists into `workspace`
  * vrq_search3_finish -- K2, exact merge of those lists + Phases II/III + the sorts
- * (same arguments as vrq_search3; the workspace carries the lists between them). */
+ * (same arguments as vrq_search3, the same flags to both; the workspace carries the lists
+ * between them). */
 int vrq_search3_scan(const uint8_t* codes, int64_t n, int32_t dim, const uint8_t* qb, int32_t nq,
-                     int32_t K, void* workspace, size_t workspace_bytes, void* stream);
+                     int32_t K, int32_t flags, void* workspace, size_t workspace_bytes, void* stream);
 int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* norms,
                        const int64_t* rescore_row, int64_t n, int32_t dim, int64_t row_offset,
                        const float* qf, int32_t nq, int32_t k, int32_t K, int32_t K3, int32_t flags,

@@ -33,9 +33,11 @@ def test_library_exports_every_declared_symbol():
 
 def test_workspace_sizes():
     lib = N.load()
-    # nq * nchunks * K * 8 bytes; deterministic in the call shape
+    # deterministic in the call shape; covers both Phase-I scans (chunk lists nq * nchunks * K * 8
+    # for the wavefront scan; prefix lists + suffix list + candidate lists for the matrix-core scan)
     ws = lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 100)
-    assert ws > 0 and ws % (1024 * 100 * 8) == 0
+    assert ws >= 1024 * 4096 * 8 and ws % 8 == 0
+    assert lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 500) % (1024 * 500 * 8) == 0  # wavefront only
     assert ws == lib.vrq_hamming_topk_workspace_size(1_000_000, 128, 1024, 100)
     assert lib.vrq_search3_workspace_size(1000, 512, 1, 10) == 0      # dim unsupported
     assert lib.vrq_hamming_topk_workspace_size(10, 128, 1, 2000) == 0  # K > 1024

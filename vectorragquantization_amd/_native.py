@@ -20,6 +20,11 @@ VRQ_EWORKSPACE = -4
 
 VRQ_SEARCH_PHASE1_ONLY = 1
 VRQ_SEARCH_SHARD = 2
+VRQ_SEARCH_SCAN_VALU = 4
+VRQ_SEARCH_SCAN_MFMA = 8
+VRQ_SCAN_STAGE_PREFIX = 16
+VRQ_SCAN_STAGE_MATRIX = 32
+VRQ_SCAN_STAGE_SUFFIX = 64
 
 ENC_MODES = {
     "int8g": 0,   # VectorDBInt8Global
@@ -41,7 +46,7 @@ SIGNATURES = {
     "vrq_search3_workspace_size": (_SZ, [_I64, _I32, _I32, _I32]),
     "vrq_search3": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _P, _I32, _I32, _I32, _I32, _I32,
                               _P, _P, _P, _P, _P, _P, _SZ, _P]),
-    "vrq_search3_scan": (C.c_int, [_P, _I64, _I32, _P, _I32, _I32, _P, _SZ, _P]),
+    "vrq_search3_scan": (C.c_int, [_P, _I64, _I32, _P, _I32, _I32, _I32, _P, _SZ, _P]),
     "vrq_search3_finish": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _I32, _I32,
                                      _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "vrq_merge_shards": (C.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),

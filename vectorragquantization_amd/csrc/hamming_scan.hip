@@ -359,7 +359,8 @@ int scan_plan(int64_t n, int cb, int nq, int K, ScanPlan* p) {
   cr = (cr + 63) & ~int64_t(63);
   // the merge (select_rescore.hip) takes at most 4096 lists per query
   if ((n + cr - 1) / cr > 4096) cr = ((n + 4095) / 4096 + 63) & ~int64_t(63);
-  if (cr > (int64_t(1) << LOCAL_BITS)) return VRQ_EUNSUPPORTED;
+  if (cr > (int64_t(1) << LOCAL_BITS)) cr = int64_t(1) << LOCAL_BITS;  // large batches: more chunks
+  if ((n + cr - 1) / cr > 4096) return VRQ_EUNSUPPORTED;                // n > 2^32 rows
   p->chunk_rows = cr;
   p->nchunks = (int)((n + cr - 1) / cr);
   p->list_bytes = (size_t)nq * p->nchunks * K * sizeof(uint64_t);

@@ -336,16 +336,26 @@ __device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, 
   if (tid == 0) a.out_count[qi] = m;
 }
 
+// Per-query lists of the scan: nlp chunk lists [nq][nlp][K], optionally followed by one
+// more list per query from a separate [nq][K] array (the matrix-core scan's suffix list,
+// whose rows all follow the prefix lists' rows).
+struct ScanKeys {
+  const uint64_t* lists;
+  const uint64_t* suffix;
+  int nlpK;
+  __device__ uint64_t operator[](int i) const { return i < nlpK ? lists[i] : suffix[i - nlpK]; }
+};
+
 // mode: 0 = full 3-phase; 1 = Phase I only; 2 = shard (all Kp candidates, s2 + s3, Phase-I order)
 __global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
-    const uint64_t* __restrict__ lists, int nl, int K, const uint8_t* __restrict__ codes,
-    const int8_t* __restrict__ x8, const double* __restrict__ norms, const float* __restrict__ qf, int mode,
-    FinishArgs fa) {
+    const uint64_t* __restrict__ lists, int nlp, const uint64_t* __restrict__ suffix, int K,
+    const uint8_t* __restrict__ codes, const int8_t* __restrict__ x8, const double* __restrict__ norms,
+    const float* __restrict__ qf, int mode, FinishArgs fa) {
   __shared__ SelShared sh;
   const int qi = blockIdx.x;
   const int tid = threadIdx.x, w = tid / WAVE, l = lane_id();
-  const uint64_t* Lq = lists + (int64_t)qi * nl * K;
-  const int Kp = select_topk(Lq, nl, K, sh);
+  const ScanKeys Lq{lists + (int64_t)qi * nlp * K, suffix ? suffix + (int64_t)qi * K : nullptr, nlp * K};
+  const int Kp = select_topk(Lq, nlp + (suffix ? 1 : 0), K, sh);
   if (mode == 1) {
     for (int i = tid; i < fa.kout; i += SEL_THREADS) {
       const int64_t o = (int64_t)qi * fa.kout + i;
@@ -471,6 +481,9 @@ size_t vrq_search3_workspace_size(int64_t n, int32_t dim, int32_t nq, int32_t K)
   if (n < 1 || nq < 1 || K < 1 || dim != DIM) return 0;
   ScanPlan p;
   if (scan_plan(n, dim / 8, nq, K, &p) != VRQ_OK) return 0;
+  MfmaPlan mp;
+  if (K <= kMfmaMaxK && n >= 2 * kMfmaMinPrefix && mfma_plan(n, nq, K, &mp) == VRQ_OK)
+    return mp.bytes > p.list_bytes ? mp.bytes : p.list_bytes;
   return p.list_bytes;
 }
 
@@ -478,6 +491,9 @@ size_t vrq_hamming_topk_workspace_size(int64_t n, int32_t code_bytes, int32_t nq
   if (n < 1 || nq < 1 || k < 1) return 0;
   ScanPlan p;
   if (scan_plan(n, code_bytes, nq, k, &p) != VRQ_OK) return 0;
+  MfmaPlan mp;
+  if (code_bytes == 128 && mfma_use(n, nq, k, 0) && mfma_plan(n, nq, k, &mp) == VRQ_OK)
+    return mp.bytes > p.list_bytes ? mp.bytes : p.list_bytes;
   return p.list_bytes;
 }
 
@@ -502,32 +518,52 @@ int vrq_hamming_topk(const uint8_t* codes, int64_t n, int32_t code_bytes, int64_
   if (nq == 0) return VRQ_OK;
   if (n == 0 || k == 0) return fill_empty(nq, k, nullptr, out_rows, out_dist, nullptr, nullptr, s);
   VRQ_CHECK_ARG(codes && queries && workspace);
-  ScanPlan p;
-  int rc = scan_plan(n, code_bytes, nq, k, &p);
-  if (rc != VRQ_OK) return rc;
-  if (workspace_bytes < p.list_bytes) return VRQ_EWORKSPACE;
-  if (p.nchunks > MAX_LISTS) return VRQ_EUNSUPPORTED;
-  uint64_t* lists = (uint64_t*)workspace;
-  rc = scan_launch(p, codes, n, code_bytes, queries, nq, k, lists, s);
-  if (rc != VRQ_OK) return rc;
   FinishArgs fa{};
   fa.row_offset = row_offset;
   fa.out_rows = out_rows;
   fa.out_dist = out_dist;
   fa.kout = k;
-  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, lists, p.nchunks, k, nullptr,
-                     nullptr, nullptr, nullptr, 1, fa);
+  uint64_t* lists = (uint64_t*)workspace;
+  if (code_bytes == 128 && mfma_use(n, nq, k, 0)) {
+    MfmaPlan mp;
+    int rc = mfma_plan(n, nq, k, &mp);
+    if (rc != VRQ_OK) return rc;
+    if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
+    rc = mfma_scan_launch(mp, codes, n, queries, nq, k, (uint8_t*)workspace, s, 0);
+    if (rc != VRQ_OK) return rc;
+    hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, lists, mp.prefix_plan.nchunks,
+                       (const uint64_t*)((uint8_t*)workspace + mp.off_suffix), k, nullptr, nullptr, nullptr, nullptr,
+                       1, fa);
+    VRQ_LAUNCH_CHECK();
+    return VRQ_OK;
+  }
+  ScanPlan p;
+  int rc = scan_plan(n, code_bytes, nq, k, &p);
+  if (rc != VRQ_OK) return rc;
+  if (workspace_bytes < p.list_bytes) return VRQ_EWORKSPACE;
+  if (p.nchunks > MAX_LISTS) return VRQ_EUNSUPPORTED;
+  rc = scan_launch(p, codes, n, code_bytes, queries, nq, k, lists, s);
+  if (rc != VRQ_OK) return rc;
+  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, lists, p.nchunks, nullptr, k,
+                     nullptr, nullptr, nullptr, nullptr, 1, fa);
   VRQ_LAUNCH_CHECK();
   return VRQ_OK;
 }
 
 int vrq_search3_scan(const uint8_t* codes, int64_t n, int32_t dim, const uint8_t* qb, int32_t nq, int32_t K,
-                     void* workspace, size_t workspace_bytes, void* stream) {
+                     int32_t flags, void* workspace, size_t workspace_bytes, void* stream) {
   VRQ_CHECK_ARG(n >= 0 && nq >= 0 && K >= 0);
   if (dim != DIM) return VRQ_EUNSUPPORTED;
   if (K > KMAX) return VRQ_EUNSUPPORTED;
   if (nq == 0 || n == 0 || K == 0) return VRQ_OK;
   VRQ_CHECK_ARG(codes && qb && workspace);
+  if (mfma_use(n, nq, K, flags)) {
+    MfmaPlan mp;
+    const int rc = mfma_plan(n, nq, K, &mp);
+    if (rc != VRQ_OK) return rc;
+    if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
+    return mfma_scan_launch(mp, codes, n, qb, nq, K, (uint8_t*)workspace, (hipStream_t)stream, flags);
+  }
   ScanPlan p;
   int rc = scan_plan(n, dim / 8, nq, K, &p);
   if (rc != VRQ_OK) return rc;
@@ -554,10 +590,22 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
     return fill_empty(nq, kout, out_count, out_rows, out_dist, out_binary, out_cosine, s);
   VRQ_CHECK_ARG(codes && workspace);
   if (mode != 1) VRQ_CHECK_ARG(qf && x8 && norms);
-  ScanPlan p;
-  int rc = scan_plan(n, dim / 8, nq, K, &p);
-  if (rc != VRQ_OK) return rc;
-  if (workspace_bytes < p.list_bytes) return VRQ_EWORKSPACE;
+  int nlp;
+  const uint64_t* suffix = nullptr;
+  if (mfma_use(n, nq, K, flags)) {
+    MfmaPlan mp;
+    const int rc = mfma_plan(n, nq, K, &mp);
+    if (rc != VRQ_OK) return rc;
+    if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
+    nlp = mp.prefix_plan.nchunks;
+    suffix = (const uint64_t*)((const uint8_t*)workspace + mp.off_suffix);
+  } else {
+    ScanPlan p;
+    const int rc = scan_plan(n, dim / 8, nq, K, &p);
+    if (rc != VRQ_OK) return rc;
+    if (workspace_bytes < p.list_bytes) return VRQ_EWORKSPACE;
+    nlp = p.nchunks;
+  }
   FinishArgs fa{};
   fa.x8 = x8;
   fa.norms = norms;
@@ -571,8 +619,8 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
   fa.out_s2 = out_binary;
   fa.out_s3 = out_cosine;
   fa.kout = kout;
-  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, (const uint64_t*)workspace,
-                     p.nchunks, K, codes, x8, norms, qf, mode, fa);
+  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, (const uint64_t*)workspace, nlp,
+                     suffix, K, codes, x8, norms, qf, mode, fa);
   VRQ_LAUNCH_CHECK();
   return VRQ_OK;
 }
@@ -585,7 +633,7 @@ int vrq_search3(const uint8_t* codes, const int8_t* x8, const double* norms, con
   const int mode = (flags & VRQ_SEARCH_PHASE1_ONLY) ? 1 : (flags & VRQ_SEARCH_SHARD) ? 2 : 0;
   const bool empty = n == 0 || K == 0 || (mode == 0 && k == 0);
   if (!empty && nq > 0) {
-    const int rc = vrq_search3_scan(codes, n, dim, qb, nq, K, workspace, workspace_bytes, stream);
+    const int rc = vrq_search3_scan(codes, n, dim, qb, nq, K, flags, workspace, workspace_bytes, stream);
     if (rc != VRQ_OK) return rc;
   }
   return vrq_search3_finish(codes, x8, norms, rescore_row, n, dim, row_offset, qf, nq, k, K, K3, flags, out_count,

@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/vrq.h"
+
 namespace vrq {
 
 // Waves the scan aims to launch (256 CUs x 16): enough to fill every SIMD several
@@ -27,5 +29,26 @@ struct ScanPlan {
 int scan_plan(int64_t n, int cb, int nq, int K, ScanPlan* p);
 int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, const uint8_t* q, int nq, int K,
                 uint64_t* lists, hipStream_t s);
+
+// ---- K1m: matrix-core scan for large query batches (hamming_mfma.hip) ----
+constexpr int kMfmaMaxK = 128;           // K bound of the path (expected suffix candidates ~15 K per query)
+constexpr int64_t kMfmaMinPrefix = 32768;
+constexpr int kMfmaMinQueries = 128;     // auto-selection threshold on the batch size
+
+struct MfmaPlan {
+  int64_t prefix;      // rows [0, prefix) scanned exactly by K1 -> tau(q)
+  int capc;            // candidate capacity per (query, chunk) list
+  int nqb;             // 256-query blocks
+  int64_t chunk_rows;  // suffix rows per workgroup (multiple of 64)
+  int nchunks;
+  int nl;              // lists handed to the select step: prefix chunk lists + 1 suffix list
+  ScanPlan prefix_plan;
+  size_t off_suffix, off_cand, off_cnt, off_tau, bytes;
+};
+
+int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p);
+bool mfma_use(int64_t n, int nq, int K, int flags);
+int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
+                     uint8_t* ws, hipStream_t s, int flags);
 
 }  // namespace vrq
