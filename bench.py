@@ -22,6 +22,7 @@ rank 0 prints ONE JSON line (see README of the driver contract).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import math
@@ -46,6 +47,8 @@ HBM_PEAK_GBS = 8000.0                          # MI355X spec (MI355X_MICROARCH.m
 # saturated (measured: tools/probes/valu_probe.hip, profiles/r1_valu_probe.json) ->
 # 1024 SIMDs x 64 lanes / 4 cycles x 2.4 GHz = 39.3 T lane-ops/s
 VALU_PEAK_TOPS = 1024 * 64 / 4 * 2.4e9 / 1e12
+# dense FP4 MFMA peak (MI355X_MICROARCH.md: ~10 PF dense): 1024 SIMDs x 4096 ops/clk x 2.4 GHz
+MFMA_FP4_PEAK_TOPS = 1024 * 4096 * 2.4e9 / 1e12
 
 
 def parse():
@@ -64,6 +67,8 @@ def parse():
     ap.add_argument("--recall-sample", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
+    ap.add_argument("--scan", choices=["auto", "valu", "mfma"], default="auto",
+                    help="Phase-I scan (auto = the library's choice for the shape)")
     return ap.parse_args()
 
 
@@ -72,9 +77,15 @@ def log(*a):
 
 
 class Pipeline:
-    """One rank's search step with event-bracketed kernels on torch's current stream."""
+    """One rank's search step with event-bracketed kernels on torch's current stream.
 
-    def __init__(self, codes, x8, norms, row0, n_total, qf, qb, k, osb, osi, world, phase1_only=False):
+    Phase I runs the scan the library selects for this shape (``vrq_scan_kind``).  For the
+    matrix-core scan its three stages are issued as three calls (``VRQ_SCAN_STAGE_*``) -- the
+    same launches in the same order as one call -- so the dominant kernel
+    (hamming_mfma_kernel) gets its own HIP events."""
+
+    def __init__(self, codes, x8, norms, row0, n_total, qf, qb, k, osb, osi, world, phase1_only=False,
+                 scan="auto"):
         self.lib = N.load()
         self.codes, self.x8, self.norms, self.row0 = codes, x8, norms, row0
         self.qf, self.qb = qf, qb
@@ -82,9 +93,14 @@ class Pipeline:
         self.world = world
         self.phase1 = phase1_only
         self.flags = N.VRQ_SEARCH_PHASE1_ONLY if phase1_only else (N.VRQ_SEARCH_SHARD if world > 1 else 0)
+        self.flags |= {"auto": 0, "valu": N.VRQ_SEARCH_SCAN_VALU, "mfma": N.VRQ_SEARCH_SCAN_MFMA}[scan]
         nq = qf.shape[0]
         dev = codes.device
         self.m = codes.shape[0]
+        pre = ctypes.c_int64(0)
+        self.kind = self.lib.vrq_scan_kind(self.m, 1024, nq, self.K, self.flags, ctypes.byref(pre))
+        N.check(min(self.kind, 0), "vrq_scan_kind")
+        self.prefix_rows = int(pre.value)
         ws = self.lib.vrq_search3_workspace_size(self.m, 1024, nq, self.K)
         self.ws = torch.empty((max(ws, 8),), dtype=torch.uint8, device=dev)
         self.list_bytes = ws
@@ -94,26 +110,35 @@ class Pipeline:
         self.dist = torch.empty((nq, kout), dtype=torch.int32, device=dev)
         self.s2 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
         self.s3 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
-        self.ids = None
         self.ev = []
         self.final = None
 
+    def _scan(self, extra, st):
+        N.check(self.lib.vrq_search3_scan(N.ptr(self.codes), self.m, 1024, N.ptr(self.qb), self.qb.shape[0],
+                                          self.K, self.flags | extra, N.ptr(self.ws), self.ws.numel(), st), "scan")
+
     def step(self, record: bool):
         L, st = self.lib, N.stream_handle(self.codes.device)
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
-        if record:
-            e[0].record()
-        N.check(L.vrq_search3_scan(N.ptr(self.codes), self.m, 1024, N.ptr(self.qb), self.qb.shape[0], self.K,
-                                   self.flags, N.ptr(self.ws), self.ws.numel(), st), "scan")
-        if record:
-            e[1].record()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if record else None
+        rec = (lambda i: e[i].record()) if record else (lambda i: None)
+        rec(0)
+        if self.kind == N.VRQ_SCAN_KIND_MFMA:
+            self._scan(N.VRQ_SCAN_STAGE_PREFIX, st)
+            rec(1)
+            self._scan(N.VRQ_SCAN_STAGE_MATRIX, st)
+            rec(2)
+            self._scan(N.VRQ_SCAN_STAGE_SUFFIX, st)
+        else:
+            self._scan(0, st)
+            rec(1)
+            rec(2)
+        rec(3)
         N.check(L.vrq_search3_finish(N.ptr(self.codes), N.ptr(self.x8), N.ptr(self.norms), None, self.m, 1024,
                                      self.row0, N.ptr(self.qf), self.qf.shape[0], self.k, self.K, self.K3,
                                      self.flags, N.ptr(self.cnt), N.ptr(self.rows), N.ptr(self.dist),
                                      N.ptr(self.s2), N.ptr(self.s3), N.ptr(self.ws), self.ws.numel(), st),
                 "finish")
-        if record:
-            e[2].record()
+        rec(4)
         if self.world > 1 and not self.phase1:
             nq = self.qf.shape[0]
             ids = self.rows  # external id = global row for the synthetic corpus
@@ -122,15 +147,17 @@ class Pipeline:
             self.final = merge_shards(gc, gr, gd, g2, g3, self.k, self.K3)
         else:
             self.final = (self.cnt, self.rows, self.dist, self.s2, self.s3)
+        rec(5)
         if record:
-            e[3].record()
             self.ev.append(e)
 
-    def kernel_ms(self):
-        sc = [a.elapsed_time(b) for a, b, _, _ in self.ev]
-        fi = [b.elapsed_time(c) for _, b, c, _ in self.ev]
-        co = [c.elapsed_time(d) for _, _, c, d in self.ev]
-        return float(np.mean(sc)), float(np.mean(fi)), float(np.mean(co))
+    def stage_ms(self):
+        """Mean ms per step of: scan (all stages), prefix stage, matrix stage, suffix stage,
+        finish (K2), all-gather + merge."""
+        def mean(i, j):
+            return float(np.mean([ev[i].elapsed_time(ev[j]) for ev in self.ev]))
+        return {"scan": mean(0, 3), "prefix": mean(0, 1), "matrix": mean(1, 2), "suffix": mean(2, 3),
+                "finish": mean(3, 4), "collective": mean(4, 5)}
 
 
 def recall_at_10(top_rows, qf, n_total, rank, world, dev, sample):
@@ -210,15 +237,25 @@ def cpu_baseline(codes_h, x8_h, qf_h, qb_h, k, osb, osi, threads, sample, gpu_ro
             "phase1_s": t1 - t0, "phase23_s": t2 - t1}, parity
 
 
-def pmc_traffic(tag):
-    """Per-launch HBM bytes of the scan kernel from a committed rocprofv3 --pmc summary
-    (FETCH_SIZE KB x2 for gfx950 16-B streams + WRITE_SIZE KB), or None."""
+def pmc_traffic(tag, kernel):
+    """Per-launch HBM bytes of `kernel` from a committed rocprofv3 --pmc summary under profiles/
+    (FETCH_SIZE KiB x2 for gfx950 16-B-per-lane streams + WRITE_SIZE KiB; tools/summarize_profile.py),
+    or None when no summary for this workload tag is committed."""
     files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*{tag}*pmc*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
-        return float(d["scan_bytes_per_launch"])
+        return float(d["bytes_per_launch"][kernel])
+    except Exception:
+        return None
+
+
+def measured_mfma_peak():
+    """Sustained FP4 MFMA rate measured by tools/probes/mfma_rate_probe (profiles/), or None."""
+    try:
+        d = json.load(open(os.path.join(HERE, "profiles", "r1_mfma_rate.json")))
+        return float(d["mfma_scale_f32_32x32x64_fp4"]["TOPS"])
     except Exception:
         return None
 
@@ -255,7 +292,8 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
 
-    P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, phase1)
+    P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, phase1,
+                 a.scan)
     for _ in range(a.warmup):
         P.step(False)
     torch.cuda.synchronize()
@@ -273,7 +311,6 @@ def main():
         tt = torch.tensor([T], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
-    scan_ms, fin_ms, coll_ms = P.kernel_ms()
 
     top_rows = P.final[1]
     rec = None
@@ -288,15 +325,33 @@ def main():
 
     m = codes.shape[0]
     K = P.K
-    alg_bytes = m * 128 + nq * 128 + nq * K * 12
-    achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
+    st = P.stage_ms()
     tag = f"{a.config}_n{n}_nq{nq}_g{world}"
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(tag), "kernel": "hamming_scan_kernel (K1)",
-            "kernel_ms": scan_ms, "algorithmic_bytes_per_launch": alg_bytes}
-    valu_ops = nq * m * 64  # 32 v_xor + 32 v_bcnt lane-ops per (query, 1024-bit row)
-    roof_valu = {"bound": "valu", "achieved": valu_ops / (scan_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS,
-                 "unit": "T lane-ops/s", "frac": valu_ops / (scan_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS}
+    # whole Phase-I scan against HBM: algorithmic bytes = corpus codes + queries + K keys/query
+    scan_bytes = m * 128 + nq * 128 + nq * K * 12
+    roof_scan_hbm = {"bound": "hbm", "achieved": scan_bytes / (st["scan"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": scan_bytes / (st["scan"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "scope": "all Phase-I stages", "ms": st["scan"], "algorithmic_bytes": scan_bytes}
+    if P.kind == N.VRQ_SCAN_KIND_MFMA:
+        # dominant kernel: hamming_mfma_kernel over rows [prefix, m): one 1024-bit AND-popcount
+        # = 1024 MACs = 2048 ops per (query, row), real queries only (padding not counted)
+        rows_m = m - P.prefix_rows
+        ops = 2048.0 * nq * rows_m
+        ach = ops / (st["matrix"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
+                "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, "hamming_mfma_kernel"),
+                "kernel": "hamming_mfma_kernel (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
+                "kernel_ms": st["matrix"], "algorithmic_ops_per_launch": ops,
+                "algorithmic_bytes_per_launch": rows_m * 128 + nq * 128,
+                "measured_sustained_peak": measured_mfma_peak(), "rows": rows_m,
+                "prefix_rows_exact_scan": P.prefix_rows}
+        roof_valu = None
+    else:
+        roof = dict(roof_scan_hbm, traffic=pmc_traffic(tag, "hamming_scan_kernel"),
+                    kernel="hamming_scan_kernel (wavefront popcount)", kernel_ms=st["scan"])
+        valu_ops = nq * m * 64  # 32 v_xor + 32 v_bcnt lane-ops per (query, 1024-bit row)
+        roof_valu = {"bound": "valu", "achieved": valu_ops / (st["scan"] * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS,
+                     "unit": "T lane-ops/s", "frac": valu_ops / (st["scan"] * 1e-3) / 1e12 / VALU_PEAK_TOPS}
     out = {
         "metric": METRIC, "value": nq * a.steps / T, "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True,
@@ -310,8 +365,8 @@ def main():
                    "int8_oversample": a.int8_oversample, "parallelism": f"row-shard x{world} + RCCL all_gather"
                    if world > 1 else "1 GPU"},
         "recall_at_10": rec,
-        "phase_ms": {"scan_K1": scan_ms, "finish_K2": fin_ms, "allgather_merge": coll_ms},
-        "roofline": roof, "roofline_valu": roof_valu,
+        "phase_ms": st, "scan_kind": "mfma" if P.kind == N.VRQ_SCAN_KIND_MFMA else "valu",
+        "roofline": roof, "roofline_scan_hbm": roof_scan_hbm, "roofline_valu": roof_valu,
     }
     if world == 1 and not a.no_cpu_baseline and not phase1:
         cb, parity = cpu_baseline(codes.cpu().numpy(), x8.cpu().numpy(), qf.cpu().numpy(), qb.cpu().numpy(),

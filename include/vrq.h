@@ -122,6 +122,14 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
                        int32_t* out_count, int64_t* out_rows, int32_t* out_dist, double* out_binary,
                        double* out_cosine, const void* workspace, size_t workspace_bytes, void* stream);
 
+/* Which Phase-I scan vrq_search3 / vrq_search3_scan / vrq_hamming_topk would run for this
+ * shape and flags: VRQ_SCAN_KIND_VALU (wavefront popcount) or VRQ_SCAN_KIND_MFMA (matrix
+ * core; *prefix_rows, if non-NULL, receives the rows scanned exactly for the threshold), or a
+ * negative VRQ_E* code for an unsupported shape.  Host-only, no device work. */
+#define VRQ_SCAN_KIND_VALU 0
+#define VRQ_SCAN_KIND_MFMA 1
+int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* prefix_rows);
+
 /* ---------------------------------------------------------------------------
  * Merge of per-shard candidate tuples after the RCCL all-gather (multi-GPU
  * row sharding; the reference is single-process, so this reproduces the

@@ -163,3 +163,21 @@ def test_mfma_and_valu_three_phase_identical(dev):
         outs[name] = [x.cpu().numpy() for x in o]
     for a, b, c in zip(outs["valu"], outs["mfma"], outs["auto"]):
         assert np.array_equal(a, b, equal_nan=True) and np.array_equal(a, c, equal_nan=True)
+
+
+def test_mfma_hit_staging_overflow(dev, oracle_lib):
+    """64 queries (one wave's worth) and the whole suffix clustered around one code: every tile
+    gives a wave ~4096 hits, more than its LDS staging holds, so the lists are marked overflowed
+    and those queries are rescanned exactly; the other queries keep the fast path."""
+    rng = np.random.default_rng(17)
+    n, nq, K = 100_000, 200, 100
+    S = 32_768
+    base = rng.integers(0, 256, (1, 128), dtype=np.uint8)
+    codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    codes[S:] = _near(rng, np.repeat(base, n - S, axis=0), 6)
+    qb = rng.integers(0, 256, (nq, 128), dtype=np.uint8)
+    qb[:64] = _near(rng, np.repeat(base, 64, axis=0), 4)
+    D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
+    _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
+    assert np.array_equal(D0, D1)
+    assert np.array_equal(I0, I1)

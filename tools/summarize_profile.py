@@ -12,6 +12,12 @@ import sys
 
 
 def short(name):
+    if "hamming_mfma" in name:
+        return "hamming_mfma_kernel"
+    if "prefix_tau" in name:
+        return "prefix_tau_kernel"
+    if "suffix_topk" in name:
+        return "suffix_topk_kernel"
     if "hamming_scan" in name:
         return "hamming_scan_kernel"
     if "select_rescore" in name:
@@ -36,19 +42,21 @@ def main(src, dst, tag):
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         out["kernel_stats"] = [r for r in csv.DictReader(open(stats[0]))]
-    for name in ("pmc_sq", "pmc_fetch", "pmc_write"):
+    for name in ("pmc_sq", "pmc_mfma", "pmc_fetch", "pmc_write"):
         f = glob.glob(os.path.join(src, name, "*counter_collection.csv"))
         if f:
             out[name] = pmc(f[0])
-    scan = "hamming_scan_kernel"
-    try:
-        fetch = out["pmc_fetch"][scan]["FETCH_SIZE"] * 1024 * 2
-        write = out["pmc_write"][scan]["WRITE_SIZE"] * 1024
-        out["scan_bytes_per_launch"] = fetch + write
-        out["scan_fetch_bytes_corrected"] = fetch
-        out["scan_write_bytes"] = write
-    except KeyError:
-        pass
+    # per-launch HBM bytes of every kernel seen by both traffic passes
+    out["bytes_per_launch"] = {}
+    for k in out.get("pmc_fetch", {}):
+        try:
+            fetch = out["pmc_fetch"][k]["FETCH_SIZE"] * 1024 * 2
+            write = out["pmc_write"][k]["WRITE_SIZE"] * 1024
+        except KeyError:
+            continue
+        out["bytes_per_launch"][k] = fetch + write
+    if "hamming_scan_kernel" in out["bytes_per_launch"]:
+        out["scan_bytes_per_launch"] = out["bytes_per_launch"]["hamming_scan_kernel"]
     json.dump(out, open(dst, "w"), indent=1)
     print("wrote", dst)
 

@@ -25,6 +25,8 @@ VRQ_SEARCH_SCAN_MFMA = 8
 VRQ_SCAN_STAGE_PREFIX = 16
 VRQ_SCAN_STAGE_MATRIX = 32
 VRQ_SCAN_STAGE_SUFFIX = 64
+VRQ_SCAN_KIND_VALU = 0
+VRQ_SCAN_KIND_MFMA = 1
 
 ENC_MODES = {
     "int8g": 0,   # VectorDBInt8Global
@@ -49,6 +51,7 @@ SIGNATURES = {
     "vrq_search3_scan": (C.c_int, [_P, _I64, _I32, _P, _I32, _I32, _I32, _P, _SZ, _P]),
     "vrq_search3_finish": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _I32, _I32,
                                      _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "vrq_scan_kind": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
     "vrq_merge_shards": (C.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "vrq_rescore_binary": (C.c_int, [_P, _I32, _I32, _P, _I64, _P, _I32, _P, _P]),
     "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),

@@ -48,7 +48,8 @@ constexpr int NPK = 4;                      // packed ring depth (DMA issued 4 t
 constexpr int NUB = 3;                      // unpacked ring: tile t read, t+1 ready, t+2 written
 constexpr int UBT = 2 * KS * 1024;          // unpacked tile bytes (32 KiB)
 constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per tile (2)
-constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + 2 * MWAVES * 64 * 4;
+constexpr int STG = 448;                    // per-wave LDS staging of candidate hits
+constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * 64 * 4 + MWAVES * STG * 12;
 constexpr int E8M0_TWO = 128;               // MX block scale 2^1
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
 
@@ -96,6 +97,12 @@ __device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
 __device__ __forceinline__ void lds_write128(uint32_t a, const v4i& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+__device__ __forceinline__ void lds_write64(uint32_t a, uint64_t v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_read64(uint64_t& d, uint32_t a) {
+  asm volatile("ds_read_b64 %0, %1" : "=v"(d) : "v"(a) : "memory");
+}
 __device__ __forceinline__ void lds_write32(uint32_t a, int v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
@@ -114,8 +121,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   int32_t* pcr = (int32_t*)(smem + NPK * PKT + NUB * UBT);  // NUB x 64 row popcounts
   // tau(q) - pc(q) per wave, [m][h][g]: the query of accumulator register g in lane-half h
   int32_t* taul = pcr + NUB * RT + (threadIdx.x >> 6) * 64;
-  // running lengths of this wave's per-(query, chunk) candidate lists, same layout
-  int32_t* lcl = pcr + NUB * RT + MWAVES * 64 + (threadIdx.x >> 6) * 64;
+  // per-wave hit staging: STG keys (u64) then STG destination offsets (u32)
+  uint8_t* stg = (uint8_t*)(pcr + NUB * RT + MWAVES * 64) + (threadIdx.x >> 6) * STG * 12;
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l = lane_id();
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
                                        (__attribute__((address_space(3))) void*)(buf + gi * 1024), 16, 0, 0);
     }
   };
-  const uint32_t pk0 = lds_addr(pk), ub0 = lds_addr(ub), pcr0 = lds_addr(pcr), lcl0 = lds_addr(lcl);
+  const uint32_t pk0 = lds_addr(pk), ub0 = lds_addr(ub), pcr0 = lds_addr(pcr);
   // unit u of this wave = (nblk, piece) = ((4w+u) >> 3, (4w+u) & 7): lane -> tile row
   // 32*nblk + ri; piece p (dwords 4p..4p+3) holds k-steps 2p, 2p+1; lane-half h takes dword
   // 2j+h of step 2p+j.
@@ -206,7 +213,6 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(A[m][s]));
-  lcl[l] = 0;
   __syncthreads();
   // accumulator seed tau'/2 per register: after the K loop acc = <q,r> + tau'/2, and the row is
   // a candidate iff pc(r) - 2<q,r> < tau'  <=>  acc > pc(r)/2
@@ -263,52 +269,65 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     mx = fmaxf(mx, a[15]);
     return __ballot(mx > half_pc);
   };
-  auto block_hits = [&](const v16f& a, int m, int pc, float half_pc, int64_t row) {
-    const uint64_t rowbits = (uint64_t)row;
-    const uint32_t la = lcl0 + (uint32_t)((m * 2 + h) * 64);
-    v4i lv[4];
+  // list lengths in registers: lcr[m][g] of lane-half h = list of query (g&3)+8(g>>2)+4h of
+  // M-block m (uniform per half); stride between consecutive queries' lists in cand
+  int lcr[2][16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds_read128(lv[i], la + 16 * i);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lv[0]), "+v"(lv[1]), "+v"(lv[2]), "+v"(lv[3])::"memory");
-    int lc[16];
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      lc[4 * i] = lv[i].x;
-      lc[4 * i + 1] = lv[i].y;
-      lc[4 * i + 2] = lv[i].z;
-      lc[4 * i + 3] = lv[i].w;
+    for (int g = 0; g < 16; ++g) lcr[m][g] = 0;
+  const int64_t qstride = (int64_t)nchunks * capc;
+  // this wave's lists: query qbase + ql, chunk `chunk` -> cbase + ql * qstride + pos
+  uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;
+  // Hits are staged in LDS and written to HBM after the end-of-tile DMA wait: a global store
+  // issued between a tile's DMA and that wait would make vmcnt wait for the DMA just issued.
+  const uint32_t stk0 = lds_addr(stg), sto0 = stk0 + STG * 8;
+  int nst = 0;  // staged entries (wave-uniform)
+  auto flush = [&]() {
+    for (int i0 = 0; i0 < nst; i0 += 64) {
+      const int i = i0 + l;
+      uint64_t key = 0;
+      int off = -1;
+      if (i < nst) {
+        lds_read64(key, stk0 + (uint32_t)(i * 8));
+        lds_read32(off, sto0 + (uint32_t)(i * 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(key), "+v"(off)::"memory");
+      if (i < nst && off >= 0) cbase[off] = key;
     }
+    nst = 0;
+  };
+  // hits of registers g0..g0+7 of a block (the any-test already found one in the block)
+  auto block_hits = [&](const v16f& a, int m, int g0, int pc, float half_pc, int64_t row) {
+    const uint64_t rowbits = (uint64_t)row;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = g0; g < g0 + 8; ++g) {
       const bool hit = a[g] > half_pc;
       const uint64_t mask = __ballot(hit);
       if (mask) {
         const uint32_t lo = (uint32_t)mask, hi = (uint32_t)(mask >> 32);
         const int below = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0));
-        const int pos = lc[g] + (h ? below - __popc(lo) : below);
-        if (hit && pos < capc) {
-          const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-          const int v = pc - 2 * (int)(a[g] - seed[m][g]);  // exact integers
-          cand[((int64_t)q * nchunks + chunk) * capc + pos] =
-              ((uint64_t)(uint32_t)(v + 1024) << KEY_ROW_BITS) | rowbits;
+        const int pos = lcr[m][g] + (h ? below - __popc(lo) : below);
+        const int cnt = __popc(lo) + __popc(hi);
+        if (nst + cnt <= STG) {
+          if (hit) {
+            const int v = pc - 2 * (int)(a[g] - seed[m][g]);  // exact integers
+            const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+            lds_write64(stk0 + (uint32_t)((nst + below) * 8),
+                        ((uint64_t)(uint32_t)(v + 1024) << KEY_ROW_BITS) | rowbits);
+            lds_write32(sto0 + (uint32_t)((nst + below) * 4), pos < capc ? (int)(ql * qstride + pos) : -1);
+          }
+          lcr[m][g] += __popc(h ? hi : lo);
+          nst += cnt;
+        } else {
+          // staging full (> STG hits in one tile): mark the list overflowed; the suffix step
+          // rescans this query exactly
+          lcr[m][g] = capc + 1;
         }
-        lc[g] += __popc(h ? hi : lo);
       }
     }
-    if (ri == 0) {  // lanes 0 and 32 write back their half's lengths
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        lds_write128(la + 16 * i, (v4i){lc[4 * i], lc[4 * i + 1], lc[4 * i + 2], lc[4 * i + 3]});
-    }
-    wait_lgkm0();
   };
-  auto block_epilogue = [&](const v16f& a, int m, int pcv, int lr) {
-    const int pc = lr < nrows ? pcv : 0x40000000;  // a row past the chunk end never hits
-    const float hp = 0.5f * (float)pc;
-    if (VRQ_BISECT & 1) return;
-    if (block_any(a, hp)) block_hits(a, m, pc, hp, row0 + lr);
-  };
-
+  auto block_pc = [&](int pcv, int lr) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
   // ---- main loop: 16 regions of 4 chained MFMAs per tile ----
   // Region r computes k-steps 4(r&3)..+3 of block b = r>>2 = (m, nbk) = (b>>1, b&1) into
   // acc[b&1]; the B fragment of each MFMA is read 2 regions ahead into a 4-slot ring (across
@@ -336,6 +355,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     lds_read32(pcvN[0], pcr0 + (uint32_t)(((t % NUB) * RT + ri) * 4));
     lds_read32(pcvN[1], pcr0 + (uint32_t)(((t % NUB) * RT + 32 + ri) * 4));
     v4i pv, pa, pb;
+    uint64_t anyb = 0;
     VRQ_SCHED_FENCE();
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -374,13 +394,21 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(pa), "+v"(pb)::"memory");
         if (!(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
       }
-      // epilogue of the previous block (block 3 of tile t-1 at region 1)
-      if ((r & 3) == 1) {
-        if (bk == 0) {
-          if (t > 0) block_epilogue(acc[1], 1, pcvP[1], (t - 1) * RT + 32 + ri);
-        } else {
-          const int pb_ = bk - 1;
-          block_epilogue(acc[pb_ & 1], pb_ >> 1, pcvN[pb_ & 1], t * RT + (pb_ & 1) * 32 + ri);
+      // epilogue of the previous block pb (block 3 of tile t-1 in regions 1-3): any-test in
+      // region 4bk+1, hits of registers 0-7 / 8-15 in regions 4bk+2 / 4bk+3
+      if ((r & 3) >= 1 && !(VRQ_BISECT & 1)) {
+        const bool prev_tile = bk == 0;
+        const int pb_ = prev_tile ? 3 : bk - 1;
+        if (!prev_tile || t > 0) {
+          const v16f& pa_ = acc[pb_ & 1];
+          const int mm = pb_ >> 1, nbk = pb_ & 1;
+          const int lr = (prev_tile ? (t - 1) : t) * RT + nbk * 32 + ri;
+          const int pc = block_pc(prev_tile ? pcvP[1] : pcvN[nbk], lr);
+          const float hp = 0.5f * (float)pc;
+          if ((r & 3) == 1)
+            anyb = block_any(pa_, hp);
+          else if (anyb)
+            block_hits(pa_, mm, ((r & 3) - 2) * 8, pc, hp, row0 + lr);
         }
       }
       VRQ_SCHED_FENCE();
@@ -393,17 +421,27 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     else
       wait_vm<0>();
     wait_lgkm0();
-    barrier_all();  // B_{t+1}
+    if (nst) flush();  // this tile's hits -> HBM; they drain while the next tile runs
+    barrier_all();     // B_{t+1}
   }
-  if (ntiles > 0) block_epilogue(acc[1], 1, pcvP[1], (ntiles - 1) * RT + 32 + ri);  // block 3, last tile
-
-  {
-    int v;
-    lds_read32(v, lcl0 + (uint32_t)(l * 4));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v)::"memory");
-    const int m = l >> 5, hh = (l >> 4) & 1, g = l & 15;  // lane -> slot [m][hh][g]
-    const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh;
-    if (q < nq) ccnt[(int64_t)q * nchunks + chunk] = v;
+  if (ntiles > 0 && !(VRQ_BISECT & 1)) {  // block 3 of the last tile
+    const int lr = (ntiles - 1) * RT + 32 + ri;
+    const int pc = block_pc(pcvP[1], lr);
+    const float hp = 0.5f * (float)pc;
+    if (block_any(acc[1], hp)) {
+      block_hits(acc[1], 1, 0, pc, hp, row0 + lr);
+      block_hits(acc[1], 1, 8, pc, hp, row0 + lr);
+    }
+  }
+  if (nst) flush();
+  if (ri == 0) {  // lanes 0 and 32 hold their half's lengths
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+        if (q < nq) ccnt[(int64_t)q * nchunks + chunk] = lcr[m][g];
+      }
   }
 }
 

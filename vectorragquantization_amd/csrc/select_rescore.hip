@@ -640,6 +640,23 @@ int vrq_search3(const uint8_t* codes, const int8_t* x8, const double* norms, con
                             out_rows, out_dist, out_binary, out_cosine, workspace, workspace_bytes, stream);
 }
 
+int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* prefix_rows) {
+  if (n < 1 || nq < 1 || K < 1) return VRQ_EINVAL;
+  if (dim != DIM || K > KMAX) return VRQ_EUNSUPPORTED;
+  if (mfma_use(n, nq, K, flags)) {
+    MfmaPlan mp;
+    const int rc = mfma_plan(n, nq, K, &mp);
+    if (rc != VRQ_OK) return rc;
+    if (prefix_rows) *prefix_rows = mp.prefix;
+    return VRQ_SCAN_KIND_MFMA;
+  }
+  ScanPlan p;
+  const int rc = scan_plan(n, dim / 8, nq, K, &p);
+  if (rc != VRQ_OK) return rc;
+  if (prefix_rows) *prefix_rows = n;
+  return VRQ_SCAN_KIND_VALU;
+}
+
 int vrq_merge_shards(int32_t nshards, int32_t nq, int32_t K, const int32_t* counts, const int64_t* rows,
                      const int32_t* dist, const double* s2, const double* s3, int32_t k, int32_t K3,
                      int32_t* out_count, int64_t* out_rows, int32_t* out_dist, double* out_binary,
