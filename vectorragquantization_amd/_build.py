@@ -20,6 +20,9 @@ SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode
 ARCH = os.environ.get("VRQ_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# per-source extras: the matrix-core scan keeps MFMA accumulators in VGPRs (the epilogue reads
+# them there; the AGPR form costs 16 v_accvgpr moves per accumulator use)
+EXTRA = {"hamming_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _hipcc() -> str:
@@ -49,7 +52,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src):
         obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *CFLAGS, *EXTRA.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -3,26 +3,33 @@
 // The wavefront popcount scan (hamming_scan.hip) costs 64 wave64 VALU instructions per
 // (query, 1024-bit row) pair and a wave64 integer VALU op retires every 4 cycles
 // (tools/probes/valu_probe.hip): beyond ~16 queries per pass it is VALU-bound.  Here the
-// same distances come from v_mfma_i32_32x32x32_i8 on 0/1 bytes:
+// same distances come from the block-scaled FP4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4) on
+// 0/1 e2m1 values:
 //     dist(q, r) = popcount(q) + popcount(r) - 2 * <bits(q), bits(r)>
-// which is exact (integer accumulation), so Phase-I ranks stay bit-identical to FAISS.
+// which is exact (integer values in f32), so Phase-I ranks stay bit-identical to FAISS.
 //
-// Work decomposition: one 256-thread workgroup per CU (LDS ~152 KiB), one wave per SIMD so
-// each wave owns the full 512-entry register file:
+// Work decomposition: one 256-thread workgroup per CU (LDS ~138 KiB), one wave per SIMD:
 //  * each wave holds the A fragments of 64 queries (2 M-blocks of 32) for the whole K = 1024
-//    (256 registers, unpacked once) and their thresholds;
+//    in the accumulator register file (128 AGPRs, unpacked once) and their thresholds folded
+//    into the accumulator seeds; accumulators, seeds and the B ring live in VGPRs, so the
+//    epilogue reads results where the MFMA wrote them;
 //  * 64-row tiles of PACKED codes stream HBM -> LDS by LDS-DMA (XOR-swizzled source, ring of
-//    3); while the matrix core runs tile t, the same waves expand tile t+1 into int8 0/1
-//    B fragments laid out [n-block][k-step][lane][16 B] (each MFMA operand read is one
-//    contiguous ds_read_b128) and the rows' popcounts -- VALU work issued in the gaps between
-//    MFMAs.  One barrier per tile hands the unpacked tile over (double buffer).
-//  * Epilogue per tile: v = pcr - 2*acc compared against tau'(q) = tau(q) - pcq(q); a row is
-//    a candidate iff dist < tau(q), where tau(q) is the exact K-th smallest distance of the
-//    query over a PREFIX of the corpus (computed by the exact scan).  FAISS admits a row only
-//    if dist < heap_top, rows in increasing index: a suffix row with dist >= tau(q) ranks
-//    after >= K prefix rows, so the strict test loses nothing.  Candidates are appended to a
-//    per-(query, chunk) list owned by one wave (ballot/mbcnt positions, no atomics);
-//    suffix_topk_kernel merges them into one sorted K-list per query, exactly in every case.
+//    4); while the matrix core runs tile t, the same waves expand tile t+2 into FP4 B
+//    fragments laid out [n-block][k-step][lane][16 B] (one contiguous ds_read_b128 per
+//    fragment) plus the rows' popcounts -- VALU work in the gaps between MFMAs.  One barrier
+//    per tile publishes the unpacked tile (ring of 3);
+//  * each B fragment feeds the MFMAs of BOTH M-blocks (LDS reads: 32 KiB per wave per tile);
+//  * epilogue per n-block, in the next n-block's MFMA shadow: a row is a candidate iff
+//    dist < tau(q), tau(q) = the exact K-th smallest distance of the query over a PREFIX of
+//    the corpus (computed by the exact scan).  FAISS admits a row only if dist < heap_top,
+//    rows in increasing index: a suffix row with dist >= tau(q) ranks after >= K prefix rows,
+//    so the strict test loses nothing.  A max3 tree + one compare per (M-block, lane) rejects
+//    hit-free blocks; hits are ballot-compacted into a per-wave LDS stage of packed 32-bit
+//    entries and, once per tile, appended to per-(query, chunk) lists in HBM at positions
+//    taken from per-query LDS counters.  suffix_topk_kernel merges the lists into one sorted
+//    K-list per query, exactly in every case (overflow -> exact rescan).
+#include <type_traits>
+
 #include "vrq_internal.h"
 #include "vrq_scan.h"
 
@@ -39,19 +46,32 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int MWAVES = 4;                   // waves per workgroup (one per SIMD)
-constexpr int QPW = 64;                     // queries per wave
+constexpr int QPW = 64;                     // queries per wave (2 M-blocks of 32)
 constexpr int QPB = MWAVES * QPW;           // queries per workgroup (256)
 constexpr int RT = 64;                      // rows per tile (2 n-blocks of 32)
 constexpr int KS = 16;                      // k-steps of 64 bits (1024-bit codes)
+constexpr int NG = 2 * KS;                  // k-step groups per tile (n-block, k-step)
 constexpr int PKT = RT * 128;               // packed tile bytes (8 KiB)
 constexpr int NPK = 4;                      // packed ring depth (DMA issued 4 tiles ahead)
 constexpr int NUB = 3;                      // unpacked ring: tile t read, t+1 ready, t+2 written
-constexpr int UBT = 2 * KS * 1024;          // unpacked tile bytes (32 KiB)
+constexpr int UBT = NG * 1024;              // unpacked tile bytes (32 KiB)
 constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per tile (2)
-constexpr int STG = 448;                    // per-wave LDS staging of candidate hits
-constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * 64 * 4 + MWAVES * STG * 12;
+constexpr int BAHEAD = 3;                   // B fragments read this many groups ahead (ring of 4)
+constexpr int STG = 512;                    // per-wave staged hit entries (u32)
+constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * QPW * 4 + MWAVES * (STG + 1) * 4;
 constexpr int E8M0_TWO = 128;               // MX block scale 2^1
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
+static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
+
+// compile-time loop: f(integral_constant<int, I>) for I in [I0, N) -- every index a constant,
+// so register arrays indexed by it stay in registers (a #pragma unroll may give up)
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
 
 __device__ __forceinline__ void barrier_all() { asm volatile("s_barrier" ::: "memory"); }
 template <int N>
@@ -62,19 +82,22 @@ __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0
 
 // 32 code bits -> one FP4 MFMA fragment lane: 32 e2m1 values, code 0x1 (0.5) per set bit.
 // Dword j, nibble i holds bit 4i + j: a fixed permutation of k applied identically to queries
-// (A) and rows (B), so every dot product is unchanged.  Two ops per dword.
-__device__ __forceinline__ v8i unpack32(uint32_t bits) {
-  v8i r = {0, 0, 0, 0, 0, 0, 0, 0};
-  r[0] = (int)(bits & 0x11111111u);
-  r[1] = (int)((bits >> 1) & 0x11111111u);
-  r[2] = (int)((bits >> 2) & 0x11111111u);
-  r[3] = (int)((bits >> 3) & 0x11111111u);
+// (A) and rows (B), so every dot product is unchanged.
+__device__ __forceinline__ v4i unpack32(uint32_t bits) {
+  v4i r;
+  r.x = (int)(bits & 0x11111111u);
+  r.y = (int)((bits >> 1) & 0x11111111u);
+  r.z = (int)((bits >> 2) & 0x11111111u);
+  r.w = (int)((bits >> 3) & 0x11111111u);
   return r;
 }
 
-// (0.5 * 2^1) * (0.5 * 2^1) = 1 per common set bit: C + popcount(q & r) exactly (<= 1024 in f32)
-__device__ __forceinline__ v16f mfma_fp4(const v8i& a, const v8i& b, const v16f& c) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, FMT_FP4, FMT_FP4, 0, E8M0_TWO, 0, E8M0_TWO);
+// (0.5 * 2^1) * (0.5 * 2^1) = 1 per common set bit: C + popcount(q & r) exactly (<= 1024 in f32).
+// FP4 operands occupy 4 registers; the upper half of the 8-register operand is ignored.
+__device__ __forceinline__ v16f mfma_fp4(const v4i& a, const v4i& b, const v16f& c) {
+  const v8i a8 = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
+  const v8i b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, FMT_FP4, FMT_FP4, 0, E8M0_TWO, 0, E8M0_TWO);
 }
 
 // LDS accesses inside the tile loop are inline asm: after a global_load_lds the compiler
@@ -87,29 +110,43 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 __device__ __forceinline__ void lds_read128(v4i& d, uint32_t a) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
-template <int OFF>
-__device__ __forceinline__ void lds_read128o(v4i& d, uint32_t a) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF) : "memory");
-}
 __device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
 __device__ __forceinline__ void lds_write128(uint32_t a, const v4i& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
-__device__ __forceinline__ void lds_write64(uint32_t a, uint64_t v) {
-  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_read64(uint64_t& d, uint32_t a) {
-  asm volatile("ds_read_b64 %0, %1" : "=v"(d) : "v"(a) : "memory");
-}
 __device__ __forceinline__ void lds_write32(uint32_t a, int v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add32(uint32_t a, int v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add_rtn32(int& d, uint32_t a, int v) {
+  asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(v) : "memory");
 }
 #define VRQ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // Packed tile image: 16-byte piece c of tile row r lives at slot r*8 + (c ^ ((r>>1)&7)).
 __device__ __forceinline__ int pk_slot(int r, int c) { return r * 8 + (c ^ ((r >> 1) & 7)); }
+
+// wave-uniform "any lane has a value > thr in these 16 registers"
+__device__ __forceinline__ bool any_above(const v16f& a, float thr) {
+  float mx = fmaxf(fmaxf(a[0], a[1]), a[2]);
+  mx = fmaxf(fmaxf(mx, a[3]), a[4]);
+  mx = fmaxf(fmaxf(mx, a[5]), a[6]);
+  mx = fmaxf(fmaxf(mx, a[7]), a[8]);
+  mx = fmaxf(fmaxf(mx, a[9]), a[10]);
+  mx = fmaxf(fmaxf(mx, a[11]), a[12]);
+  mx = fmaxf(fmaxf(mx, a[13]), a[14]);
+  mx = fmaxf(mx, a[15]);
+  return __ballot(mx > thr) != 0;
+}
+
+// Staged hit entry (u32): (v + 1024) << 13 | query-in-wave << 7 | row - (t-1)*64, where
+// v = dist - pc(q) in [-1024, 1024] and the row is relative to the previous tile's first row
+// (the epilogue of a tile's second n-block runs in the next tile's iteration).
+constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
 
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
@@ -119,12 +156,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
   int32_t* pcr = (int32_t*)(smem + NPK * PKT + NUB * UBT);  // NUB x 64 row popcounts
-  // tau(q) - pc(q) per wave, [m][h][g]: the query of accumulator register g in lane-half h
-  int32_t* taul = pcr + NUB * RT + (threadIdx.x >> 6) * 64;
-  // per-wave hit staging: STG keys (u64) then STG destination offsets (u32)
-  uint8_t* stg = (uint8_t*)(pcr + NUB * RT + MWAVES * 64) + (threadIdx.x >> 6) * STG * 12;
-
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int32_t* lcnt = pcr + NUB * RT + w * QPW;                 // this wave's 64 list lengths
+  int32_t* stg = pcr + NUB * RT + MWAVES * QPW + w * (STG + 1);  // this wave's hit staging (+1 spare)
+
   const int l = lane_id();
   const int h = l >> 5, ri = l & 31;
   // XCD-aware bijective remap: consecutive logical blocks share one XCD's L2
@@ -155,9 +190,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
   };
   const uint32_t pk0 = lds_addr(pk), ub0 = lds_addr(ub), pcr0 = lds_addr(pcr);
+  const uint32_t lc0 = lds_addr(lcnt), stg0 = lds_addr(stg);
   // unit u of this wave = (nblk, piece) = ((4w+u) >> 3, (4w+u) & 7): lane -> tile row
   // 32*nblk + ri; piece p (dwords 4p..4p+3) holds k-steps 2p, 2p+1; lane-half h takes dword
-  // 2j+h of step 2p+j.
+  // 2j+h of step 2p+j.  Unpacked layout [n-block][k-step][lane][16 B]: group g = 16*nblk + s.
   uint32_t usrc[4], udst[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -170,9 +206,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   const int pr = 16 * w + (l >> 2), pc0 = 2 * (l & 3);
   const uint32_t psrc0 = (uint32_t)(pk_slot(pr, pc0) * 16), psrc1 = (uint32_t)(pk_slot(pr, pc0 + 1) * 16);
   auto unpack_write = [&](const v4i& v, int u, uint32_t ubuf) {
-    const v8i f0 = unpack32((uint32_t)(h ? v.y : v.x)), f1 = unpack32((uint32_t)(h ? v.w : v.z));
-    lds_write128(ubuf + udst[u], (v4i){f0[0], f0[1], f0[2], f0[3]});
-    lds_write128(ubuf + udst[u] + 1024, (v4i){f1[0], f1[1], f1[2], f1[3]});
+    lds_write128(ubuf + udst[u], unpack32((uint32_t)(h ? v.y : v.x)));
+    lds_write128(ubuf + udst[u] + 1024, unpack32((uint32_t)(h ? v.w : v.z)));
   };
   auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) {
     int pc = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(c.x) + __popc(c.y) + __popc(c.z) +
@@ -186,7 +221,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int t = 0; t < NPK && t < ntiles; ++t) issue(t);
 
   const int qbase = qb * QPB + w * QPW;
-  v8i A[2][KS];  // [m][s]: bits 64s+32h .. +31 of query qbase + 32m + ri as 32 e2m1 values
+  v4i A[2][KS];  // [m][s]: bits 64s+32h .. +31 of query qbase + 32m + ri as 32 e2m1 values
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int q = qbase + 32 * m + ri;
@@ -201,18 +236,21 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       A[m][2 * c] = unpack32(h ? wd[1] : wd[0]);
       A[m][2 * c + 1] = unpack32(h ? wd[3] : wd[2]);
     }
-    // lane (ri, h=0) holds query ri's threshold; slot [m][h'][g] wants query (g&3)+8(g>>2)+4h'
+    // lane (ri, h=0) holds query ri's threshold; slot [m][h'][g] wants query (g&3)+8(g>>2)+4h'.
+    // The wave's staging area holds the 64 thresholds until the first hit.
     const int tl = qok ? tau[q] - pc : -0x40000000;  // padded queries never accept
     if (h == 0) {
       const int g = (ri & 3) | ((ri >> 3) << 2);     // inverse of (g&3) + 8(g>>2)
-      taul[(m * 2 + ((ri >> 2) & 1)) * 16 + g] = tl;
+      stg[(m * 2 + ((ri >> 2) & 1)) * 16 + g] = tl;
     }
   }
-  // A lives in the accumulator file (MFMA reads it from there), freeing the VGPRs for the B ring
+  // A lives in the accumulator file (the MFMA reads it from there); VGPRs hold the
+  // accumulators, seeds and the B ring
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(A[m][s]));
+  lcnt[l] = 0;
   __syncthreads();
   // accumulator seed tau'/2 per register: after the K loop acc = <q,r> + tau'/2, and the row is
   // a candidate iff pc(r) - 2<q,r> < tau'  <=>  acc > pc(r)/2
@@ -220,7 +258,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int g = 0; g < 16; ++g) seed[m][g] = 0.5f * (float)taul[(m * 2 + h) * 16 + g];
+    for (int g = 0; g < 16; ++g) seed[m][g] = 0.5f * (float)stg[(m * 2 + h) * 16 + g];
 
   if (ntiles >= 4)
     wait_vm<2 * GPW>();
@@ -228,7 +266,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     wait_vm<GPW>();
   else
     wait_vm<0>();
-  barrier_all();  // packed tiles 0 and 1 visible to all waves
+  barrier_all();  // packed tiles 0 and 1 visible to all waves; thresholds read
   {
     v4i pv[8], pa[2], pb[2];
 #pragma unroll
@@ -254,195 +292,146 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     wait_vm<0>();
   wait_lgkm0();
 
-  // ---- epilogue helpers: block (m, nbk) of a finished tile ----
-  // accumulator register g = query (g&3)+8(g>>2)+4h of M-block m, tile row 32*nbk + ri.
-  // A hit stores key (v + 1024) << 40 | row with v = pc(row) - 2<q,row> = dist - pc(q) (the
-  // same order as dist for a fixed query).
-  auto block_any = [&](const v16f& a, float half_pc) -> uint64_t {
-    float mx = fmaxf(fmaxf(a[0], a[1]), a[2]);
-    mx = fmaxf(fmaxf(mx, a[3]), a[4]);
-    mx = fmaxf(fmaxf(mx, a[5]), a[6]);
-    mx = fmaxf(fmaxf(mx, a[7]), a[8]);
-    mx = fmaxf(fmaxf(mx, a[9]), a[10]);
-    mx = fmaxf(fmaxf(mx, a[11]), a[12]);
-    mx = fmaxf(fmaxf(mx, a[13]), a[14]);
-    mx = fmaxf(mx, a[15]);
-    return __ballot(mx > half_pc);
-  };
-  // list lengths in registers: lcr[m][g] of lane-half h = list of query (g&3)+8(g>>2)+4h of
-  // M-block m (uniform per half); stride between consecutive queries' lists in cand
-  int lcr[2][16];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int g = 0; g < 16; ++g) lcr[m][g] = 0;
+  // ---- hit path ----
   const int64_t qstride = (int64_t)nchunks * capc;
   // this wave's lists: query qbase + ql, chunk `chunk` -> cbase + ql * qstride + pos
   uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;
-  // Hits are staged in LDS and written to HBM after the end-of-tile DMA wait: a global store
-  // issued between a tile's DMA and that wait would make vmcnt wait for the DMA just issued.
-  const uint32_t stk0 = lds_addr(stg), sto0 = stk0 + STG * 8;
   int nst = 0;  // staged entries (wave-uniform)
-  auto flush = [&]() {
+  // staged entries -> per-(query, chunk) lists in HBM.  Runs after the end-of-tile DMA wait: a
+  // global store issued between a tile's DMA and that wait would make vmcnt wait for the DMA.
+  auto flush = [&](int64_t base_row) {
+    if (nst > STG) {  // staging overflowed in this tile: every list of the wave -> exact rescan
+      lds_add32(lc0 + (uint32_t)(l * 4), capc + 1);
+      nst = STG;
+    }
     for (int i0 = 0; i0 < nst; i0 += 64) {
       const int i = i0 + l;
-      uint64_t key = 0;
-      int off = -1;
-      if (i < nst) {
-        lds_read64(key, stk0 + (uint32_t)(i * 8));
-        lds_read32(off, sto0 + (uint32_t)(i * 4));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(key), "+v"(off)::"memory");
-      if (i < nst && off >= 0) cbase[off] = key;
+      int e = 0, pos = 0;
+      if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+      const int ql = (e >> ENT_Q_SHIFT) & 63;
+      if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+      if (i < nst && pos < capc)
+        cbase[ql * qstride + pos] = ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) |
+                                    (uint64_t)(base_row + (e & 127));
     }
     nst = 0;
   };
-  // hits of registers g0..g0+7 of a block (the any-test already found one in the block)
-  auto block_hits = [&](const v16f& a, int m, int g0, int pc, float half_pc, int64_t row) {
-    const uint64_t rowbits = (uint64_t)row;
+  // hits of block (m, n-block) whose rows are rel7 = row - (t-1)*64.  A block with a hit sends
+  // all 16 compares out first (VALU -> SGPR lane masks) so the wave pays one VALU->SALU latency
+  // per block, not one per register; registers without hits cost a scalar test.  Positions past STG land in a
+  // spare slot and the flush marks the whole wave's lists overflowed (exact rescan).
+  auto block_hits = [&](const v16f& a, int m, int pc, float hp, int rel7) {
+    if (!any_above(a, hp)) return;  // max3 tree + one compare: most blocks stop here
+    uint64_t mk[16];
 #pragma unroll
-    for (int g = g0; g < g0 + 8; ++g) {
-      const bool hit = a[g] > half_pc;
-      const uint64_t mask = __ballot(hit);
-      if (mask) {
-        const uint32_t lo = (uint32_t)mask, hi = (uint32_t)(mask >> 32);
-        const int below = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0));
-        const int pos = lcr[m][g] + (h ? below - __popc(lo) : below);
-        const int cnt = __popc(lo) + __popc(hi);
-        if (nst + cnt <= STG) {
-          if (hit) {
-            const int v = pc - 2 * (int)(a[g] - seed[m][g]);  // exact integers
-            const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-            lds_write64(stk0 + (uint32_t)((nst + below) * 8),
-                        ((uint64_t)(uint32_t)(v + 1024) << KEY_ROW_BITS) | rowbits);
-            lds_write32(sto0 + (uint32_t)((nst + below) * 4), pos < capc ? (int)(ql * qstride + pos) : -1);
-          }
-          lcr[m][g] += __popc(h ? hi : lo);
-          nst += cnt;
-        } else {
-          // staging full (> STG hits in one tile): mark the list overflowed; the suffix step
-          // rescans this query exactly
-          lcr[m][g] = capc + 1;
+    for (int g = 0; g < 16; ++g) mk[g] = __ballot(a[g] > hp);
+    VRQ_SCHED_FENCE();  // all compares issue back to back before the first scalar test
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if (mk[g]) {
+        const uint64_t mask = mk[g];
+        if ((mask >> l) & 1) {
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+          const int v = pc - 2 * (int)(a[g] - seed[m][g]);  // exact integers
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+          const int pos = nst + below < STG ? nst + below : STG;
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | rel7);
         }
+        nst += __popcll(mask);
       }
     }
   };
-  auto block_pc = [&](int pcv, int lr) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
-  // ---- main loop: 16 regions of 4 chained MFMAs per tile ----
-  // Region r computes k-steps 4(r&3)..+3 of block b = r>>2 = (m, nbk) = (b>>1, b&1) into
-  // acc[b&1]; the B fragment of each MFMA is read 2 regions ahead into a 4-slot ring (across
-  // the tile boundary: tile t+1 is complete before iteration t starts).  Unpack of tile t+2
-  // (one unit per 4 regions) and the epilogue of the previous block run in the MFMA shadow.
-  v4i ring[4][4];
-  v16f acc[2];
-  auto read_region = [&](int slot_, uint32_t ubuf, int r) {
-    const int bb = r >> 2, qq = r & 3, nbk = bb & 1;
-    const uint32_t base = ubuf + (uint32_t)(((nbk * KS + 4 * qq) * 64 + l) * 16);
+  auto row_pc = [&](int pcv, int lr) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
+
+  // ---- main loop: 32 groups per tile; group gi = (n-block gi>>4, k-step gi&15) runs the two
+  // MFMAs of M-blocks 0 and 1 on ONE B fragment (read BAHEAD groups ahead into a ring of 4,
+  // across the tile boundary: tile t+1 is complete before iteration t starts).  Unpack of tile
+  // t+2 (one unit per 8 groups) and the epilogue of the previous n-block run in the MFMA shadow.
+  v4i ring[4];
+  v16f acc[2][2];  // [n-block][m]
+  auto readB = [&](int slot_, uint32_t ubuf, int g) { lds_read128(ring[slot_], ubuf + (uint32_t)((g * 64 + l) * 16)); };
+  int pcvP = 0;  // previous tile's n-block 1 row popcount
+  barrier_all();  // B_0: unpacked tiles 0 and 1, packed tile 2 visible
 #pragma unroll
-    for (int j = 0; j < 4; ++j) lds_read128(ring[slot_][j], base + (uint32_t)(j * 1024));
-  };
-  int pcvP[2] = {0, 0};  // previous tile's row popcounts (block 3 = nbk 1)
-  barrier_all();         // B_0: unpacked tiles 0 and 1, packed tile 2 visible
-  read_region(0, ub0, 0);
-  read_region(1, ub0, 1);
+  for (int g = 0; g < BAHEAD; ++g) readB(g, ub0, g);
   for (int t = 0; t < ntiles; ++t) {
     if (t + 4 < ntiles) issue(t + 4);  // into the slot of tile t (unpacked in iteration t-2)
     const uint32_t ubt = ub0 + (uint32_t)((t % NUB) * UBT);
     const uint32_t ubn = ub0 + (uint32_t)(((t + 1) % NUB) * UBT);
     const uint32_t ubw = ub0 + (uint32_t)(((t + 2) % NUB) * UBT);
     const uint32_t pks = pk0 + (uint32_t)(((t + 2) % NPK) * PKT);
-    int pcvN[2];
-    lds_read32(pcvN[0], pcr0 + (uint32_t)(((t % NUB) * RT + ri) * 4));
-    lds_read32(pcvN[1], pcr0 + (uint32_t)(((t % NUB) * RT + 32 + ri) * 4));
+    int pcv[2];
+    lds_read32(pcv[0], pcr0 + (uint32_t)(((t % NUB) * RT + ri) * 4));
+    lds_read32(pcv[1], pcr0 + (uint32_t)(((t % NUB) * RT + 32 + ri) * 4));
     v4i pv, pa, pb;
-    uint64_t anyb = 0;
     VRQ_SCHED_FENCE();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int bk = r >> 2, qq = r & 3, m = bk >> 1;
-      // B fragments of region r+2 (tile t+1 for r >= 14)
-      if (r + 2 < 16)
-        read_region((r + 2) & 3, ubt, r + 2);
+    static_for<0, NG>([&](auto GI) {
+      constexpr int gi = decltype(GI)::value;
+      constexpr int nbk = gi >> 4, s = gi & 15, j = gi & 15;
+      if constexpr (gi + BAHEAD < NG)
+        readB((gi + BAHEAD) & 3, ubt, gi + BAHEAD);
       else
-        read_region((r + 2) & 3, ubn, r + 2 - 16);
-      // packed reads two regions before their use (regions 3, 7, 11, 15 unpack; 15 row pcs)
-      if ((r & 3) == 1) lds_read128(pv, pks + usrc[r >> 2]);
-      if (r == 13) {
+        readB((gi + BAHEAD) & 3, ubn, gi + BAHEAD - NG);
+      // packed reads of the unpack units (used 4 groups later) and of the row popcounts
+      if ((gi & 7) == 1) lds_read128(pv, pks + usrc[gi >> 3]);
+      if (gi == 26) {
         lds_read128(pa, pks + psrc0);
         lds_read128(pb, pks + psrc1);
       }
-      // region r's fragments: >= 8 LDS ops were issued after them
-      asm volatile("s_waitcnt lgkmcnt(8)"
-                   : "+v"(ring[r & 3][0]), "+v"(ring[r & 3][1]), "+v"(ring[r & 3][2]), "+v"(ring[r & 3][3]),
-                     "+v"(pv), "+v"(pcvN[0]), "+v"(pcvN[1])::"memory");
-      v16f& c = acc[bk & 1];
-#pragma unroll
-      for (int j = 0; j < ((VRQ_BISECT & 4) ? 0 : 4); ++j) {
-        const int s = 4 * qq + j;
-        const v4i& bf = ring[r & 3][j];
-        const v8i bv = {bf.x, bf.y, bf.z, bf.w, 0, 0, 0, 0};
-        c = mfma_fp4(A[m][s], bv, s == 0 ? seed[m] : c);
+      // everything but the BAHEAD most recent LDS operations has completed: the fragment of
+      // this group (read BAHEAD groups ago), the packed unit read 4 groups ago, the popcounts
+      asm volatile("s_waitcnt lgkmcnt(%6)"
+                   : "+v"(ring[gi & 3]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb)
+                   : "n"(BAHEAD)
+                   : "memory");
+      if (!(VRQ_BISECT & 4)) {
+        acc[nbk][0] = mfma_fp4(A[0][s], ring[gi & 3], s == 0 ? seed[0] : acc[nbk][0]);
+        acc[nbk][1] = mfma_fp4(A[1][s], ring[gi & 3], s == 0 ? seed[1] : acc[nbk][1]);
+      } else if (s == 0) {
+        acc[nbk][0] = seed[0];
+        acc[nbk][1] = seed[1];
       }
-      if (VRQ_BISECT & 4) {
-        if (qq == 0) c = seed[m];
-      }
-      // pin the accumulator here: the MFMA intrinsics are pure, and without a use at this point
-      // IR-level sinking moves them past the scheduling fences
-      asm volatile("" : "+a"(c));
-      if ((r & 3) == 3 && !(VRQ_BISECT & 2)) unpack_write(pv, r >> 2, ubw);
-      if (r == 15) {
-        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(pa), "+v"(pb)::"memory");
-        if (!(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
-      }
-      // epilogue of the previous block pb (block 3 of tile t-1 in regions 1-3): any-test in
-      // region 4bk+1, hits of registers 0-7 / 8-15 in regions 4bk+2 / 4bk+3
-      if ((r & 3) >= 1 && !(VRQ_BISECT & 1)) {
-        const bool prev_tile = bk == 0;
-        const int pb_ = prev_tile ? 3 : bk - 1;
-        if (!prev_tile || t > 0) {
-          const v16f& pa_ = acc[pb_ & 1];
-          const int mm = pb_ >> 1, nbk = pb_ & 1;
-          const int lr = (prev_tile ? (t - 1) : t) * RT + nbk * 32 + ri;
-          const int pc = block_pc(prev_tile ? pcvP[1] : pcvN[nbk], lr);
-          const float hp = 0.5f * (float)pc;
-          if ((r & 3) == 1)
-            anyb = block_any(pa_, hp);
-          else if (anyb)
-            block_hits(pa_, mm, ((r & 3) - 2) * 8, pc, hp, row0 + lr);
-        }
+      // pin the accumulators here: the MFMA intrinsics are pure, and without a use at this
+      // point IR-level sinking moves them past the scheduling fences
+      asm volatile("" : "+v"(acc[nbk][0]), "+v"(acc[nbk][1]));
+      if ((gi & 7) == 5 && !(VRQ_BISECT & 2)) unpack_write(pv, gi >> 3, ubw);
+      if (gi == 30 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
+      // epilogue of the previous n-block (n-block 1 of tile t-1 during n-block 0, n-block 0 of
+      // tile t during n-block 1): any-tests in group 3, hits of (m, register half) in 4..7
+      if (!(VRQ_BISECT & 1) && (j == 3 || j == 5) && (nbk == 1 || t > 0)) {
+        const v16f* pa_ = acc[nbk ^ 1];
+        const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+        const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+        const int pc = row_pc(pcr_, lr);
+        constexpr int m = j == 3 ? 0 : 1;
+        block_hits(pa_[m], m, pc, 0.5f * (float)pc, (nbk == 0 ? 32 : 64) + ri);
       }
       VRQ_SCHED_FENCE();
-    }
-    pcvP[0] = pcvN[0];
-    pcvP[1] = pcvN[1];
+    });
+    pcvP = pcv[1];
     // packed tile t+3 (unpacked next iteration) landed; this wave's LDS writes done
     if (t + 4 < ntiles)
       wait_vm<GPW>();
     else
       wait_vm<0>();
     wait_lgkm0();
-    if (nst) flush();  // this tile's hits -> HBM; they drain while the next tile runs
-    barrier_all();     // B_{t+1}
+    if (nst) flush(row0 + (int64_t)(t - 1) * RT);  // hits -> HBM; they drain while the next tile runs
+    barrier_all();                                 // B_{t+1}
   }
-  if (ntiles > 0 && !(VRQ_BISECT & 1)) {  // block 3 of the last tile
+  if (ntiles > 0 && !(VRQ_BISECT & 1)) {  // n-block 1 of the last tile
     const int lr = (ntiles - 1) * RT + 32 + ri;
-    const int pc = block_pc(pcvP[1], lr);
+    const int pc = row_pc(pcvP, lr);
     const float hp = 0.5f * (float)pc;
-    if (block_any(acc[1], hp)) {
-      block_hits(acc[1], 1, 0, pc, hp, row0 + lr);
-      block_hits(acc[1], 1, 8, pc, hp, row0 + lr);
-    }
+    block_hits(acc[1][0], 0, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
+    block_hits(acc[1][1], 1, pc, hp, 96 + ri);
+    if (nst) flush(row0 + (int64_t)(ntiles - 2) * RT);
   }
-  if (nst) flush();
-  if (ri == 0) {  // lanes 0 and 32 hold their half's lengths
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-        if (q < nq) ccnt[(int64_t)q * nchunks + chunk] = lcr[m][g];
-      }
-  }
+  wait_lgkm0();
+  const int q = qbase + l;
+  if (q < nq) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
 }
 
 // Exact prefix threshold: tau(q) = K-th smallest distance over the union of the prefix
