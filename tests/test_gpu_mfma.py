@@ -181,3 +181,26 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib):
     _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
     assert np.array_equal(D0, D1)
     assert np.array_equal(I0, I1)
+
+
+def test_mfma_sampled_threshold_rerun(dev, oracle_lib):
+    """The matrix pass runs with the sampled threshold tau_s = d_(j)+1 of the prefix (j < K).
+    Queries 0 and 290 (two different 256-query blocks) have 80 near copies (dist <= 20) inside
+    the prefix and 10 more at dist 30 in the suffix, none elsewhere: d_(j) falls among the prefix
+    copies, the suffix copies miss tau_s, the check proves C < K and the re-run with tau_p must
+    recover them (plus the right dist ~420 tail).  The other queries take the fast path."""
+    rng = np.random.default_rng(23)
+    n, nq, K = 100_000, 300, 100
+    S = 32_768
+    codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    qb = _near(rng, codes[rng.integers(0, n, nq)], 50)
+    for q in (0, 290):
+        pre = rng.choice(S, 80, replace=False)
+        codes[pre] = _near(rng, np.repeat(qb[q:q + 1], 80, axis=0), int(rng.integers(5, 21)))
+        suf = S + rng.choice(n - S, 10, replace=False)
+        codes[suf] = _near(rng, np.repeat(qb[q:q + 1], 10, axis=0), 30)
+    D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
+    _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
+    assert (D0[0] == 30).sum() == 10 and (D0[290] == 30).sum() == 10
+    assert np.array_equal(D0, D1)
+    assert np.array_equal(I0, I1)

@@ -40,7 +40,7 @@ int main(int argc, char** argv) {
   for (int it = 0; it < 6; ++it) {
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL(vrq::hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes, n,
-                       p.prefix, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb);
+                       p.prefix, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb, nullptr, nullptr);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms;

@@ -34,7 +34,8 @@
 #include "vrq_scan.h"
 
 // tools/probes/mfma_bisect.hip compiles this file with VRQ_BISECT bits set to time the kernel
-// with parts removed (1: epilogue, 2: unpack, 4: MFMA).  Never set in the library build.
+// with parts removed (1: epilogue, 2: unpack, 4: MFMA, 8: tile barrier, 16: B-fragment waits;
+// 8 and 16 give wrong results, timing only).  Never set in the library build.
 #ifndef VRQ_BISECT
 #define VRQ_BISECT 0
 #endif
@@ -56,7 +57,16 @@ constexpr int NPK = 4;                      // packed ring depth (DMA issued 4 t
 constexpr int NUB = 3;                      // unpacked ring: tile t read, t+1 ready, t+2 written
 constexpr int UBT = NG * 1024;              // unpacked tile bytes (32 KiB)
 constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per tile (2)
-constexpr int BAHEAD = 3;                   // B fragments read this many groups ahead (ring of 4)
+#if VRQ_BISECT & 16
+#define VRQ_BWAIT "; no wait %7"
+#else
+#define VRQ_BWAIT "s_waitcnt lgkmcnt(%7)"
+#endif
+#ifndef VRQ_BAHEAD
+#define VRQ_BAHEAD 3
+#endif
+constexpr int BAHEAD = VRQ_BAHEAD;          // B fragments read this many groups ahead
+constexpr int NRING = BAHEAD < 4 ? 4 : 8;   // B fragment ring (power of two > BAHEAD)
 constexpr int STG = 512;                    // per-wave staged hit entries (u32)
 constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * QPW * 4 + MWAVES * (STG + 1) * 4;
 constexpr int E8M0_TWO = 128;               // MX block scale 2^1
@@ -151,7 +161,7 @@ constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
-    int64_t chunk_rows, int nchunks, int nqb) {
+    int64_t chunk_rows, int nchunks, int nqb, const int32_t* __restrict__ rerun, const int32_t* __restrict__ qbflag) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM_BYTES];
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
@@ -169,6 +179,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   const int chunk = L / nqb;
   const int qb = L - chunk * nqb;
   if (chunk >= nchunks) return;
+  // re-run pass (exact fallback of the sampled threshold): only query blocks with a failed query
+  if (qbflag && qbflag[qb] == 0) return;
   const int64_t row0 = row_begin + (int64_t)chunk * chunk_rows;
   const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
   const int nrows = (int)(row1 - row0);
@@ -225,7 +237,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int q = qbase + 32 * m + ri;
-    const bool qok = q < nq;
+    const bool qok = q < nq && (!rerun || rerun[q]);
     const uint4* qp = reinterpret_cast<const uint4*>(queries + (int64_t)(qok ? q : 0) * 128);
     int pc = 0;
 #pragma unroll
@@ -297,14 +309,30 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // this wave's lists: query qbase + ql, chunk `chunk` -> cbase + ql * qstride + pos
   uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;
   int nst = 0;  // staged entries (wave-uniform)
-  // staged entries -> per-(query, chunk) lists in HBM.  Runs after the end-of-tile DMA wait: a
-  // global store issued between a tile's DMA and that wait would make vmcnt wait for the DMA.
-  auto flush = [&](int64_t base_row) {
+  // Staged entries -> per-(query, chunk) lists in HBM.  The first 64 entries of a tile go
+  // asynchronously: read back from the stage in group 22 (all hits of a tile are staged by group
+  // 21), list positions taken by ds_add_rtn in group 26, both in the MFMA shadow; the global
+  // stores issue at the top of the next iteration, BEFORE that iteration's LDS-DMA, so the
+  // end-of-tile vmcnt wait never waits on a store issued after a DMA.  Entries past 64 (and a
+  // stage overflow) take the synchronous path at the end of the tile.
+  int fe = 0, fpos = 0, nfl = 0;
+  int64_t fbase = 0;
+  auto fkey = [&](int e, int64_t base_row) {
+    return ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) | (uint64_t)(base_row + (e & 127));
+  };
+  auto store_flushed = [&]() {
+    if (nfl) {
+      const int ql = (fe >> ENT_Q_SHIFT) & 63;
+      if (l < nfl && fpos < capc) cbase[ql * qstride + fpos] = fkey(fe, fbase);
+      nfl = 0;
+    }
+  };
+  auto flush_from = [&](int i_begin, int64_t base_row) {
     if (nst > STG) {  // staging overflowed in this tile: every list of the wave -> exact rescan
       lds_add32(lc0 + (uint32_t)(l * 4), capc + 1);
       nst = STG;
     }
-    for (int i0 = 0; i0 < nst; i0 += 64) {
+    for (int i0 = i_begin; i0 < nst; i0 += 64) {
       const int i = i0 + l;
       int e = 0, pos = 0;
       if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
@@ -312,9 +340,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       const int ql = (e >> ENT_Q_SHIFT) & 63;
       if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
-      if (i < nst && pos < capc)
-        cbase[ql * qstride + pos] = ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) |
-                                    (uint64_t)(base_row + (e & 127));
+      if (i < nst && pos < capc) cbase[ql * qstride + pos] = fkey(e, base_row);
     }
     nst = 0;
   };
@@ -350,7 +376,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // MFMAs of M-blocks 0 and 1 on ONE B fragment (read BAHEAD groups ahead into a ring of 4,
   // across the tile boundary: tile t+1 is complete before iteration t starts).  Unpack of tile
   // t+2 (one unit per 8 groups) and the epilogue of the previous n-block run in the MFMA shadow.
-  v4i ring[4];
+  v4i ring[NRING];
   v16f acc[2][2];  // [n-block][m]
   auto readB = [&](int slot_, uint32_t ubuf, int g) { lds_read128(ring[slot_], ubuf + (uint32_t)((g * 64 + l) * 16)); };
   int pcvP = 0;  // previous tile's n-block 1 row popcount
@@ -358,6 +384,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 #pragma unroll
   for (int g = 0; g < BAHEAD; ++g) readB(g, ub0, g);
   for (int t = 0; t < ntiles; ++t) {
+    store_flushed();                   // previous tile's first 64 hits
     if (t + 4 < ntiles) issue(t + 4);  // into the slot of tile t (unpacked in iteration t-2)
     const uint32_t ubt = ub0 + (uint32_t)((t % NUB) * UBT);
     const uint32_t ubn = ub0 + (uint32_t)(((t + 1) % NUB) * UBT);
@@ -372,9 +399,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       constexpr int gi = decltype(GI)::value;
       constexpr int nbk = gi >> 4, s = gi & 15, j = gi & 15;
       if constexpr (gi + BAHEAD < NG)
-        readB((gi + BAHEAD) & 3, ubt, gi + BAHEAD);
+        readB((gi + BAHEAD) & (NRING - 1), ubt, gi + BAHEAD);
       else
-        readB((gi + BAHEAD) & 3, ubn, gi + BAHEAD - NG);
+        readB((gi + BAHEAD) & (NRING - 1), ubn, gi + BAHEAD - NG);
       // packed reads of the unpack units (used 4 groups later) and of the row popcounts
       if ((gi & 7) == 1) lds_read128(pv, pks + usrc[gi >> 3]);
       if (gi == 26) {
@@ -383,13 +410,13 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       }
       // everything but the BAHEAD most recent LDS operations has completed: the fragment of
       // this group (read BAHEAD groups ago), the packed unit read 4 groups ago, the popcounts
-      asm volatile("s_waitcnt lgkmcnt(%6)"
-                   : "+v"(ring[gi & 3]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb)
+      asm volatile(VRQ_BWAIT
+                   : "+v"(ring[gi & (NRING - 1)]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb), "+v"(fe)
                    : "n"(BAHEAD)
                    : "memory");
       if (!(VRQ_BISECT & 4)) {
-        acc[nbk][0] = mfma_fp4(A[0][s], ring[gi & 3], s == 0 ? seed[0] : acc[nbk][0]);
-        acc[nbk][1] = mfma_fp4(A[1][s], ring[gi & 3], s == 0 ? seed[1] : acc[nbk][1]);
+        acc[nbk][0] = mfma_fp4(A[0][s], ring[gi & (NRING - 1)], s == 0 ? seed[0] : acc[nbk][0]);
+        acc[nbk][1] = mfma_fp4(A[1][s], ring[gi & (NRING - 1)], s == 0 ? seed[1] : acc[nbk][1]);
       } else if (s == 0) {
         acc[nbk][0] = seed[0];
         acc[nbk][1] = seed[1];
@@ -398,6 +425,12 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       // point IR-level sinking moves them past the scheduling fences
       asm volatile("" : "+v"(acc[nbk][0]), "+v"(acc[nbk][1]));
       if ((gi & 7) == 5 && !(VRQ_BISECT & 2)) unpack_write(pv, gi >> 3, ubw);
+      if constexpr (gi == 22) {  // async flush, step 1: the stage's first 64 entries
+        lds_read32(fe, stg0 + (uint32_t)(l * 4));
+        nfl = nst < 64 ? nst : 64;
+      }
+      if constexpr (gi == 26)  // step 2: list positions (idle lanes add 0)
+        lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 63) * 4), l < nfl ? 1 : 0);
       if (gi == 30 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
       // epilogue of the previous n-block (n-block 1 of tile t-1 during n-block 0, n-block 0 of
       // tile t during n-block 1): any-tests in group 3, hits of (m, register half) in 4..7
@@ -417,29 +450,42 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       wait_vm<GPW>();
     else
       wait_vm<0>();
-    wait_lgkm0();
-    if (nst) flush(row0 + (int64_t)(t - 1) * RT);  // hits -> HBM; they drain while the next tile runs
-    barrier_all();                                 // B_{t+1}
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fpos), "+v"(fe)::"memory");
+    fbase = row0 + (int64_t)(t - 1) * RT;
+    if (nst > 64) flush_from(64, fbase);  // rare: more than 64 hits in one tile
+    nst = 0;
+    if (!(VRQ_BISECT & 8)) barrier_all();  // B_{t+1}
   }
+  store_flushed();
   if (ntiles > 0 && !(VRQ_BISECT & 1)) {  // n-block 1 of the last tile
     const int lr = (ntiles - 1) * RT + 32 + ri;
     const int pc = row_pc(pcvP, lr);
     const float hp = 0.5f * (float)pc;
     block_hits(acc[1][0], 0, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
     block_hits(acc[1][1], 1, pc, hp, 96 + ri);
-    if (nst) flush(row0 + (int64_t)(ntiles - 2) * RT);
+    if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }
   wait_lgkm0();
   const int q = qbase + l;
-  if (q < nq) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
+  if (q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
 }
 
-// Exact prefix threshold: tau(q) = K-th smallest distance over the union of the prefix
-// chunk lists; 1025 (admit every suffix row) when the prefix holds fewer than K rows.
-__global__ __launch_bounds__(256) void prefix_tau_kernel(const uint64_t* __restrict__ lists, int nl, int K,
-                                                         int32_t* __restrict__ tau) {
+// Thresholds from the exact prefix lists (sorted top-K of rows [0, prefix) per query):
+//   tau_p(q) = d_(K), the K-th smallest prefix distance (1025 when the prefix holds fewer than K
+//              rows): every suffix row with dist >= tau_p ranks after >= K prefix rows, so the
+//              strict test dist < tau_p is exact (the guaranteed threshold);
+//   tau_s(q) = d_(j) + 1 for the plan's j < K (accept dist <= d_(j)): with iid rows the corpus
+//              holds ~j*n/prefix rows below it, >= K with probability 1 - 1e-6 (plan), and the
+//              check kernel proves it per query; cpre(q) = prefix rows with dist < tau_s.
+// With j >= K the plan uses tau_p alone (tau_s = tau_p, no check).
+__global__ __launch_bounds__(256) void prefix_tau_kernel(const uint64_t* __restrict__ lists, int nl, int K, int j,
+                                                         int32_t* __restrict__ tau_s, int32_t* __restrict__ tau_p,
+                                                         int32_t* __restrict__ cpre, int32_t* __restrict__ qbflag,
+                                                         int nqb) {
   __shared__ uint32_t hist[1025];
   const int qi = blockIdx.x, tid = threadIdx.x;
+  if (qi == 0 && qbflag)
+    for (int i = tid; i < nqb; i += 256) qbflag[i] = 0;
   for (int i = tid; i < 1025; i += 256) hist[i] = 0;
   __syncthreads();
   const uint64_t* Lq = lists + (int64_t)qi * nl * K;
@@ -450,8 +496,8 @@ __global__ __launch_bounds__(256) void prefix_tau_kernel(const uint64_t* __restr
   __syncthreads();
   if (tid < 64) {  // one wave: prefix sums over 1025 bins, 17 per lane
     int loc = 0;
-    for (int j = 0; j < 17; ++j) {
-      const int d = tid * 17 + j;
+    for (int i = 0; i < 17; ++i) {
+      const int d = tid * 17 + i;
       if (d < 1025) loc += (int)hist[d];
     }
     int inc = loc;
@@ -459,21 +505,59 @@ __global__ __launch_bounds__(256) void prefix_tau_kernel(const uint64_t* __restr
       const int y = __shfl_up(inc, o, 64);
       if (tid >= o) inc += y;
     }
-    int cum = inc - loc, res = 1025;
-    for (int j = 0; j < 17; ++j) {
-      const int d = tid * 17 + j;
+    // K-th and j-th smallest: bin d holds them iff cum < k <= cum + hist[d]
+    int cum = inc - loc, rk = 1025, rj = 1025, cj = 0x7fffffff;
+    for (int i = 0; i < 17; ++i) {
+      const int d = tid * 17 + i;
       if (d < 1025) {
         const int hh = (int)hist[d];
-        if (cum < K && cum + hh >= K) res = d;
+        if (cum < K && cum + hh >= K) rk = d;
+        if (cum < j && cum + hh >= j) {
+          rj = d;
+          cj = cum + hh;  // rows with dist <= d_(j)
+        }
         cum += hh;
       }
     }
-    // exactly one lane (or none) found it
+    // exactly one lane (or none) found each
     for (int o = 32; o > 0; o >>= 1) {
-      const int y = __shfl_xor(res, o, 64);
-      res = y < res ? y : res;
+      rk = min(rk, __shfl_xor(rk, o, 64));
+      rj = min(rj, __shfl_xor(rj, o, 64));
+      cj = min(cj, __shfl_xor(cj, o, 64));
     }
-    if (tid == 0) tau[qi] = res;
+    if (tid == 0) {
+      const int total = __shfl(inc, 63, 64);
+      tau_p[qi] = rk;
+      if (j >= K) {
+        tau_s[qi] = rk;
+      } else if (rj < 1025) {
+        tau_s[qi] = rj + 1;
+        cpre[qi] = cj;
+      } else {  // fewer than j prefix rows: accept everything
+        tau_s[qi] = 1025;
+        cpre[qi] = total;
+      }
+    }
+  }
+}
+
+// Proof of the sampled threshold per query: C = cpre + suffix rows with dist < tau_s (the list
+// lengths; an overflowed list counts > capc, and its exact rescan needs no threshold).  C >= K
+// means the K-th smallest key of the whole corpus has dist < tau_s, so the candidates hold the
+// exact top-K.  Otherwise the query is flagged for the re-run with tau_p.  One wave per query.
+__global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __restrict__ cpre,
+                                                           const int32_t* __restrict__ ccnt, int nchunks, int K,
+                                                           int nq, int32_t* __restrict__ rerun,
+                                                           int32_t* __restrict__ qbflag) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
+  if (q >= nq) return;
+  int64_t c = 0;
+  for (int i = l; i < nchunks; i += 64) c += ccnt[(int64_t)q * nchunks + i];
+  c = wave_sum_i64(c);
+  const bool fail = cpre[q] + c < K;
+  if (l == 0) {
+    rerun[q] = fail ? 1 : 0;
+    if (fail) atomicOr(&qbflag[q / QPB], 1);
   }
 }
 
@@ -683,9 +767,20 @@ __global__ __launch_bounds__(SUF_THREADS) void suffix_topk_kernel(const uint8_t*
   }
 }
 
+// P(Poisson(lam) >= j) <= 1e-6: the sampled order j that an iid corpus proves with that probability
+static int sample_order(double lam, int K) {
+  double term = __builtin_exp(-lam), cdf = 0.0;
+  for (int j = 1; j < K; ++j) {
+    cdf += term;  // P(X <= j-1)
+    if (1.0 - cdf <= 1e-6) return j;
+    term *= lam / j;
+  }
+  return K;
+}
+
 int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   if (nq < 1 || K < 1 || K > kMfmaMaxK) return VRQ_EUNSUPPORTED;
-  int64_t S = n / 16;
+  int64_t S = n / kMfmaPrefixDiv;
   if (S < kMfmaMinPrefix) S = kMfmaMinPrefix;
   if (S > n) S = n;
   p->prefix = S;
@@ -703,17 +798,18 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   int capc = 64;
   while (capc < 4 * expect && capc < 4096) capc <<= 1;
   p->capc = capc;
+  p->j = sample_order((double)K * (double)S / (double)n, K);
   if (scan_plan(S, 128, nq, K, &p->prefix_plan) != VRQ_OK) return VRQ_EUNSUPPORTED;
   if (p->prefix_plan.nchunks + 1 > 4096) return VRQ_EUNSUPPORTED;  // select step's list bound
   p->nl = p->prefix_plan.nchunks + 1;  // prefix chunk lists + the suffix list
   // workspace: prefix lists [nq][nlp][K] | suffix list [nq][K] | cand [nq][nchunks][capc] |
-  //            list lengths [nq][nchunks] | tau [nq]
+  //            list lengths [nq][nchunks] | tau_s, tau_p, cpre, rerun [nq] | qbflag [nqb]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   p->off_suffix = al(p->prefix_plan.list_bytes);
   p->off_cand = p->off_suffix + al((size_t)nq * K * sizeof(uint64_t));
   p->off_cnt = p->off_cand + al((size_t)nq * p->nchunks * p->capc * sizeof(uint64_t));
   p->off_tau = p->off_cnt + al((size_t)nq * p->nchunks * sizeof(int32_t));
-  p->bytes = p->off_tau + (size_t)nq * sizeof(int32_t);
+  p->bytes = p->off_tau + 4 * al((size_t)nq * sizeof(int32_t)) + (size_t)p->nqb * sizeof(int32_t);
   return VRQ_OK;
 }
 
@@ -732,17 +828,35 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   uint64_t* suffix = (uint64_t*)(ws + p.off_suffix);
   uint64_t* cand = (uint64_t*)(ws + p.off_cand);
   int32_t* ccnt = (int32_t*)(ws + p.off_cnt);
-  int32_t* tau = (int32_t*)(ws + p.off_tau);
+  const size_t qa = ((size_t)nq * sizeof(int32_t) + 255) & ~size_t(255);
+  int32_t* tau_s = (int32_t*)(ws + p.off_tau);
+  int32_t* tau_p = (int32_t*)(ws + p.off_tau + qa);
+  int32_t* cpre = (int32_t*)(ws + p.off_tau + 2 * qa);
+  int32_t* rerun = (int32_t*)(ws + p.off_tau + 3 * qa);
+  int32_t* qbflag = (int32_t*)(ws + p.off_tau + 4 * qa);
+  const bool sampled = p.j < K;
   if (st & VRQ_SCAN_STAGE_PREFIX) {
     int rc = scan_launch(p.prefix_plan, codes, p.prefix, 128, q, nq, K, lists, s);
     if (rc != VRQ_OK) return rc;
-    hipLaunchKernelGGL(prefix_tau_kernel, dim3(nq), dim3(256), 0, s, lists, p.prefix_plan.nchunks, K, tau);
+    hipLaunchKernelGGL(prefix_tau_kernel, dim3(nq), dim3(256), 0, s, lists, p.prefix_plan.nchunks, K, p.j, tau_s,
+                       tau_p, cpre, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_MATRIX) && p.nchunks > 0) {
     hipLaunchKernelGGL(hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n, p.prefix,
-                       q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb);
+                       q, nq, tau_s, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb, (const int32_t*)nullptr,
+                       (const int32_t*)nullptr);
     VRQ_LAUNCH_CHECK();
+    if (sampled) {
+      // prove C >= K per query; re-run the query blocks holding a failed query with tau_p
+      hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, cpre, ccnt, p.nchunks, K, nq,
+                         rerun, qbflag);
+      VRQ_LAUNCH_CHECK();
+      hipLaunchKernelGGL(hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+                         p.prefix, q, nq, tau_p, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb,
+                         (const int32_t*)rerun, (const int32_t*)qbflag);
+      VRQ_LAUNCH_CHECK();
+    }
   }
   if (st & VRQ_SCAN_STAGE_SUFFIX) {
     hipLaunchKernelGGL(suffix_topk_kernel, dim3(nq), dim3(SUF_THREADS), 0, s, codes, n, p.prefix, q, cand, ccnt,

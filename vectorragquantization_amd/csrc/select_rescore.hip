@@ -30,19 +30,29 @@ constexpr uint64_t ROW_MASK = (1ull << KEY_ROW_BITS) - 1;
 constexpr int DIM = 1024;           // embedding dim of the fused kernels
 constexpr int DPL = DIM / WAVE;     // dims per lane (16)
 
+// Per-query LDS state, sized for at most KM candidates (binary_k) and ML lists.  The general
+// instance (KMAX, MAX_LISTS) takes ~89 KiB, one workgroup per CU; the common shape (K <= 128,
+// <= 64 lists) runs the small instance (~11 KiB) so 8 workgroups share a CU.
+template <int KM, int ML>
 struct SelShared {
+  static constexpr int kKM = KM, kML = ML;
   uint32_t hist[NBINS];
-  int32_t ltcnt[MAX_LISTS];
-  int32_t eqend[MAX_LISTS];
-  uint64_t sel[KMAX];       // Phase-I keys (dist << 40 | row), FAISS order after select
-  int32_t pay[KMAX];        // payload index (list * K + pos) of each selected key
-  uint64_t skey[KMAX];      // sort keys (descending score image)
-  int32_t sidx[KMAX];       // sort payload (Phase-I rank)
-  double s2[KMAX];
-  double s3[KMAX];
+  int32_t ltcnt[ML];
+  int32_t eqend[ML];
+  uint64_t sel[KM];         // Phase-I keys (dist << 40 | row), FAISS order after select
+  int32_t pay[KM];          // payload index (list * K + pos) of each selected key
+  uint64_t skey[KM];        // sort keys (descending score image)
+  int32_t sidx[KM];         // sort payload (Phase-I rank)
+  double s2[KM];
+  double s3[KM];
+  int32_t ord2[KM];         // Phase-I ranks in Phase-II order (first K3)
+  double s3o[KM];           // Phase-III scores in Phase-II order
   int32_t scan[SEL_THREADS / WAVE + 1];
   int32_t misc[8];
 };
+constexpr int KSMALL = 128, LSMALL = 64;
+typedef SelShared<KMAX, MAX_LISTS> SelBig;
+typedef SelShared<KSMALL, LSMALL> SelSmall;
 
 // Block-wide exclusive scan of one int per thread; returns exclusive prefix, total in *tot.
 __device__ inline int block_excl_scan(int v, int* tot, int32_t* scratch) {
@@ -70,8 +80,8 @@ __device__ inline int block_excl_scan(int v, int* tot, int32_t* scratch) {
 // Exact top-Kp (Kp = min(K, #valid)) of the union of nl sorted lists of K keys each,
 // whose row ranges are disjoint and increasing with the list index.  Result: sh.sel[0..Kp)
 // ascending by key (= FAISS (dist, row) order) with sh.pay = list*K + pos.  Returns Kp.
-template <class KeyAt>
-__device__ int select_topk(const KeyAt& L, int nl, int K, SelShared& sh) {
+template <class KeyAt, class SH>
+__device__ int select_topk(const KeyAt& L, int nl, int K, SH& sh) {
   const int tid = threadIdx.x;
   const int total = nl * K;
   for (int i = tid; i < NBINS; i += SEL_THREADS) sh.hist[i] = 0;
@@ -197,7 +207,8 @@ __device__ int select_topk(const KeyAt& L, int nl, int K, SelShared& sh) {
 // Stable descending sort of scores sc[0..m) keeping the original positions:
 // (desc image of score, position) lexicographic -- Python's list.sort(reverse=True)
 // on a key is stable, so equal scores keep their previous order (:296, :321).
-__device__ void stable_desc_order(const double* sc, int m, SelShared& sh) {
+template <class SH>
+__device__ void stable_desc_order(const double* sc, int m, SH& sh) {
   const int np2 = next_pow2(m > 1 ? m : 1);
   for (int i = threadIdx.x; i < np2; i += SEL_THREADS) {
     sh.skey[i] = i < m ? desc_key_f64(sc[i]) : KEY_NONE;
@@ -289,12 +300,13 @@ struct FinishArgs {
   int kout;
 };
 
-__device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, SelShared& sh) {
+template <class SH>
+__device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, SH& sh) {
   const int tid = threadIdx.x, w = tid / WAVE, l = lane_id();
   stable_desc_order(sh.s2, Kp, sh);  // sh.sidx[0..Kp) = Phase-I ranks in Phase-II order
   const int K3p = a.K3 < Kp ? a.K3 : Kp;
   // stash the Phase-II order (sidx is reused by the next sort)
-  __shared__ int32_t ord2[KMAX];
+  int32_t* ord2 = sh.ord2;
   for (int i = tid; i < K3p; i += SEL_THREADS) ord2[i] = sh.sidx[i];
   __syncthreads();
   if (!have_s3) {
@@ -310,7 +322,7 @@ __device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, 
   }
   __syncthreads();
   // gather s3 in Phase-II order, stable sort desc
-  __shared__ double s3o[KMAX];
+  double* s3o = sh.s3o;
   for (int i = tid; i < K3p; i += SEL_THREADS) s3o[i] = sh.s3[ord2[i]];
   __syncthreads();
   stable_desc_order(s3o, K3p, sh);
@@ -347,11 +359,12 @@ struct ScanKeys {
 };
 
 // mode: 0 = full 3-phase; 1 = Phase I only; 2 = shard (all Kp candidates, s2 + s3, Phase-I order)
+template <class SH>
 __global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
     const uint64_t* __restrict__ lists, int nlp, const uint64_t* __restrict__ suffix, int K,
     const uint8_t* __restrict__ codes, const int8_t* __restrict__ x8, const double* __restrict__ norms,
     const float* __restrict__ qf, int mode, FinishArgs fa) {
-  __shared__ SelShared sh;
+  __shared__ SH sh;
   const int qi = blockIdx.x;
   const int tid = threadIdx.x, w = tid / WAVE, l = lane_id();
   const ScanKeys Lq{lists + (int64_t)qi * nlp * K, suffix ? suffix + (int64_t)qi * K : nullptr, nlp * K};
@@ -426,13 +439,14 @@ struct ShardKeys {
   }
 };
 
+template <class SH>
 __global__ __launch_bounds__(SEL_THREADS) void merge_shards_kernel(int S, int K, const int32_t* __restrict__ counts,
                                                                    const int64_t* __restrict__ rows,
                                                                    const int32_t* __restrict__ dist,
                                                                    const double* __restrict__ s2,
                                                                    const double* __restrict__ s3, int nq,
                                                                    FinishArgs fa) {
-  __shared__ SelShared sh;
+  __shared__ SH sh;
   const int qi = blockIdx.x;
   const int tid = threadIdx.x;
   const ShardKeys L{counts, rows, dist, nq, qi, K};
@@ -469,6 +483,21 @@ __global__ __launch_bounds__(256) void rescore_kernel(int which, const float* __
   load_q(qv, qf + (int64_t)qi * DIM);
   const double v = which == 0 ? phase2_dot(qv, codes + row * (DIM / 8)) : phase3_cos(qv, x8 + row * DIM, norms[row]);
   if (lane_id() == 0) out[gw] = v;
+}
+
+// launch the small-LDS instance when the shape fits it
+static int launch_select(hipStream_t s, int nq, const uint64_t* lists, int nlp, const uint64_t* suffix, int K,
+                         const uint8_t* codes, const int8_t* x8, const double* norms, const float* qf, int mode,
+                         const FinishArgs& fa) {
+  const int nl = nlp + (suffix ? 1 : 0);
+  if (K <= KSMALL && nl <= LSMALL)
+    hipLaunchKernelGGL(select_rescore_kernel<SelSmall>, dim3(nq), dim3(SEL_THREADS), 0, s, lists, nlp, suffix, K,
+                       codes, x8, norms, qf, mode, fa);
+  else
+    hipLaunchKernelGGL(select_rescore_kernel<SelBig>, dim3(nq), dim3(SEL_THREADS), 0, s, lists, nlp, suffix, K,
+                       codes, x8, norms, qf, mode, fa);
+  VRQ_LAUNCH_CHECK();
+  return VRQ_OK;
 }
 
 }  // namespace vrq
@@ -531,11 +560,9 @@ int vrq_hamming_topk(const uint8_t* codes, int64_t n, int32_t code_bytes, int64_
     if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
     rc = mfma_scan_launch(mp, codes, n, queries, nq, k, (uint8_t*)workspace, s, 0);
     if (rc != VRQ_OK) return rc;
-    hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, lists, mp.prefix_plan.nchunks,
-                       (const uint64_t*)((uint8_t*)workspace + mp.off_suffix), k, nullptr, nullptr, nullptr, nullptr,
-                       1, fa);
-    VRQ_LAUNCH_CHECK();
-    return VRQ_OK;
+    return launch_select(s, nq, lists, mp.prefix_plan.nchunks,
+                         (const uint64_t*)((uint8_t*)workspace + mp.off_suffix), k, nullptr, nullptr, nullptr,
+                         nullptr, 1, fa);
   }
   ScanPlan p;
   int rc = scan_plan(n, code_bytes, nq, k, &p);
@@ -544,10 +571,7 @@ int vrq_hamming_topk(const uint8_t* codes, int64_t n, int32_t code_bytes, int64_
   if (p.nchunks > MAX_LISTS) return VRQ_EUNSUPPORTED;
   rc = scan_launch(p, codes, n, code_bytes, queries, nq, k, lists, s);
   if (rc != VRQ_OK) return rc;
-  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, lists, p.nchunks, nullptr, k,
-                     nullptr, nullptr, nullptr, nullptr, 1, fa);
-  VRQ_LAUNCH_CHECK();
-  return VRQ_OK;
+  return launch_select(s, nq, lists, p.nchunks, nullptr, k, nullptr, nullptr, nullptr, nullptr, 1, fa);
 }
 
 int vrq_search3_scan(const uint8_t* codes, int64_t n, int32_t dim, const uint8_t* qb, int32_t nq, int32_t K,
@@ -619,10 +643,7 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
   fa.out_s2 = out_binary;
   fa.out_s3 = out_cosine;
   fa.kout = kout;
-  hipLaunchKernelGGL(select_rescore_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, (const uint64_t*)workspace, nlp,
-                     suffix, K, codes, x8, norms, qf, mode, fa);
-  VRQ_LAUNCH_CHECK();
-  return VRQ_OK;
+  return launch_select(s, nq, (const uint64_t*)workspace, nlp, suffix, K, codes, x8, norms, qf, mode, fa);
 }
 
 int vrq_search3(const uint8_t* codes, const int8_t* x8, const double* norms, const int64_t* rescore_row,
@@ -678,8 +699,12 @@ int vrq_merge_shards(int32_t nshards, int32_t nq, int32_t K, const int32_t* coun
   fa.out_s3 = out_cosine;
   fa.out_src = out_src;
   fa.kout = k;
-  hipLaunchKernelGGL(merge_shards_kernel, dim3(nq), dim3(SEL_THREADS), 0, s, nshards, K, counts, rows, dist, s2,
-                     s3, nq, fa);
+  if (K <= KSMALL && nshards <= LSMALL)
+    hipLaunchKernelGGL(merge_shards_kernel<SelSmall>, dim3(nq), dim3(SEL_THREADS), 0, s, nshards, K, counts, rows,
+                       dist, s2, s3, nq, fa);
+  else
+    hipLaunchKernelGGL(merge_shards_kernel<SelBig>, dim3(nq), dim3(SEL_THREADS), 0, s, nshards, K, counts, rows,
+                       dist, s2, s3, nq, fa);
   VRQ_LAUNCH_CHECK();
   return VRQ_OK;
 }

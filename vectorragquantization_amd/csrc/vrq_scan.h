@@ -34,10 +34,12 @@ int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, cons
 constexpr int kMfmaMaxK = 128;           // K bound of the path (expected suffix candidates ~15 K per query)
 constexpr int64_t kMfmaMinPrefix = 32768;
 constexpr int kMfmaMinQueries = 128;     // auto-selection threshold on the batch size
+constexpr int64_t kMfmaPrefixDiv = 16;   // exact prefix = n / kMfmaPrefixDiv rows
 
 struct MfmaPlan {
   int64_t prefix;      // rows [0, prefix) scanned exactly by K1 -> tau(q)
   int capc;            // candidate capacity per (query, chunk) list
+  int j;               // sampled threshold order (tau_s = d_(j) + 1 of the prefix); K = tau_p only
   int nqb;             // 256-query blocks
   int64_t chunk_rows;  // suffix rows per workgroup (multiple of 64)
   int nchunks;
