@@ -52,9 +52,12 @@ extern "C" {
 /* vrq_search3_scan only, matrix-core scan only: run a subset of its three stages (none set =
  * all), so a caller can bracket each stage with events; issuing the three in order on one
  * stream is exactly the full scan. */
-#define VRQ_SCAN_STAGE_PREFIX 16 /* exact scan of the prefix rows -> per-query threshold */
-#define VRQ_SCAN_STAGE_MATRIX 32 /* hamming_mfma_kernel over the suffix rows */
-#define VRQ_SCAN_STAGE_SUFFIX 64 /* suffix candidates -> one sorted list (exact rescan on overflow) */
+#define VRQ_SCAN_STAGE_PREFIX 16 /* dense matrix-core pass over a spread row sample -> per-query
+                                    thresholds (sampled d_(j), guaranteed d_(K)) */
+#define VRQ_SCAN_STAGE_MATRIX 32 /* thresholded matrix-core pass over all rows (+ per-query proof
+                                    and exact re-run of the rare failed query blocks) */
+#define VRQ_SCAN_STAGE_SUFFIX 64 /* candidates -> one sorted K-list per query (exact rescan on
+                                    list overflow) */
 
 /* encoder modes for vrq_encode */
 #define VRQ_ENC_INT8_GLOBAL 0  /* VectorDBInt8Global._quantize_to_int8 + _to_binary */
@@ -124,7 +127,8 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
 
 /* Which Phase-I scan vrq_search3 / vrq_search3_scan / vrq_hamming_topk would run for this
  * shape and flags: VRQ_SCAN_KIND_VALU (wavefront popcount) or VRQ_SCAN_KIND_MFMA (matrix
- * core; *prefix_rows, if non-NULL, receives the rows scanned exactly for the threshold), or a
+ * core; *prefix_rows, if non-NULL, receives the rows scanned outside the thresholded
+ * matrix-core pass: 0, or n for the wavefront scan), or a
  * negative VRQ_E* code for an unsupported shape.  Host-only, no device work. */
 #define VRQ_SCAN_KIND_VALU 0
 #define VRQ_SCAN_KIND_MFMA 1

@@ -97,13 +97,13 @@ def test_mfma_heavy_ties(dev, oracle_lib):
 
 
 def test_mfma_candidate_overflow_exact_rescan(dev, oracle_lib):
-    """Query 0's neighbours all sit after the prefix: > capg suffix rows beat its prefix
-    threshold, so its list overflows and the suffix is rescanned exactly.  The suffix holds 50
+    """Query 0's neighbours fill rows [S, n): far more rows beat its threshold than a candidate
+    list holds, so its lists overflow and the corpus is rescanned exactly.  Those rows hold 50
     exact copies (dist 0) and otherwise rows at dist exactly 3, so with K = 100 the answer is
     the 50 copies plus the FIRST 50 dist-3 rows in row order."""
     rng = np.random.default_rng(9)
     n, nq, K = 100_000, 130, 100
-    S = 32_768                                            # prefix rows of this n (kMfmaMinPrefix)
+    S = 32_768
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     qb = rng.integers(0, 256, (nq, 128), dtype=np.uint8)
     suffix = _near(rng, np.repeat(qb[:1], n - S, axis=0), 3)
@@ -183,24 +183,38 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib):
     assert np.array_equal(I0, I1)
 
 
+def _sample_rows(n, nq):
+    """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S =
+    max(n/32, 32768) rows in 256/nqb chunks of RT-aligned rows, chunk c at row c * (n // chunks)."""
+    nqb = (nq + 255) // 256
+    S = min(n, max(n // 32, 32768))
+    nsc = max(1, 256 // nqb)
+    scr = ((S + nsc - 1) // nsc + 63) // 64 * 64
+    nsc = (S + scr - 1) // scr
+    stride = n // nsc
+    r = np.arange(n)
+    return r[((r % stride) < scr) & (r // stride < nsc)]
+
+
 def test_mfma_sampled_threshold_rerun(dev, oracle_lib):
-    """The matrix pass runs with the sampled threshold tau_s = d_(j)+1 of the prefix (j < K).
-    Queries 0 and 290 (two different 256-query blocks) have 80 near copies (dist <= 20) inside
-    the prefix and 10 more at dist 30 in the suffix, none elsewhere: d_(j) falls among the prefix
-    copies, the suffix copies miss tau_s, the check proves C < K and the re-run with tau_p must
-    recover them (plus the right dist ~420 tail).  The other queries take the fast path."""
+    """The thresholded pass runs with the sampled tau_s = d_(j)+1 (j < K) of the dense sample.
+    Queries 0 and 290 (two different 256-query blocks) get 70 near copies (dist <= 20) on sample
+    rows and 40 more at dist 30 off the sample, none elsewhere: d_(j) falls among the near
+    copies, the dist-30 copies miss tau_s, the check finds C = 70 < K and the re-run with tau_p
+    must recover the first 30 of them in row order.  The other queries take the fast path."""
     rng = np.random.default_rng(23)
     n, nq, K = 100_000, 300, 100
-    S = 32_768
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     qb = _near(rng, codes[rng.integers(0, n, nq)], 50)
+    samp = _sample_rows(n, nq)
+    off = np.setdiff1d(np.arange(n), samp)
     for q in (0, 290):
-        pre = rng.choice(S, 80, replace=False)
-        codes[pre] = _near(rng, np.repeat(qb[q:q + 1], 80, axis=0), int(rng.integers(5, 21)))
-        suf = S + rng.choice(n - S, 10, replace=False)
-        codes[suf] = _near(rng, np.repeat(qb[q:q + 1], 10, axis=0), 30)
+        near = rng.choice(samp, 70, replace=False)
+        codes[near] = _near(rng, np.repeat(qb[q:q + 1], 70, axis=0), int(rng.integers(5, 21)))
+        far = rng.choice(off, 40, replace=False)
+        codes[far] = _near(rng, np.repeat(qb[q:q + 1], 40, axis=0), 30)
     D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
     _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
-    assert (D0[0] == 30).sum() == 10 and (D0[290] == 30).sum() == 10
+    assert (D0[0] == 30).sum() == 30 and (D0[290] == 30).sum() == 30
     assert np.array_equal(D0, D1)
     assert np.array_equal(I0, I1)

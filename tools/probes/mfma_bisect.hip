@@ -39,15 +39,16 @@ int main(int argc, char** argv) {
   float best = 1e30f;
   for (int it = 0; it < 6; ++it) {
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(vrq::hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes, n,
-                       p.prefix, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb, nullptr, nullptr);
+    hipLaunchKernelGGL(vrq::hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes,
+                       n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
     if (it > 0 && ms < best) best = ms;
   }
-  const double rows = (double)(n - p.prefix);
+  const double rows = (double)n;
   const double tiles_per_wg = (double)p.chunk_rows / vrq::RT;
   const double ops = rows * nq * 2048.0;
   printf("{\"bisect\": %d, \"n\": %lld, \"nq\": %d, \"ms\": %.4f, \"us_per_tile\": %.3f, \"TOPS\": %.1f, "

@@ -28,6 +28,8 @@
 //    entries and, once per tile, appended to per-(query, chunk) lists in HBM at positions
 //    taken from per-query LDS counters.  suffix_topk_kernel merges the lists into one sorted
 //    K-list per query, exactly in every case (overflow -> exact rescan).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "vrq_internal.h"
@@ -158,10 +160,16 @@ __device__ __forceinline__ bool any_above(const v16f& a, float thr) {
 // (the epilogue of a tile's second n-block runs in the next tile's iteration).
 constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
 
+// DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) is written
+// as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + row].  Chunk c covers
+// rows [row_begin + c * chunk_stride, + chunk_rows) (the sample spreads its chunks over the corpus;
+// the thresholded pass uses chunk_stride = chunk_rows).
+template <bool DENSE>
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
-    int64_t chunk_rows, int nchunks, int nqb, const int32_t* __restrict__ rerun, const int32_t* __restrict__ qbflag) {
+    int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, const int32_t* __restrict__ rerun,
+    const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM_BYTES];
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
@@ -181,8 +189,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   if (chunk >= nchunks) return;
   // re-run pass (exact fallback of the sampled threshold): only query blocks with a failed query
   if (qbflag && qbflag[qb] == 0) return;
-  const int64_t row0 = row_begin + (int64_t)chunk * chunk_rows;
+  const int64_t row0 = row_begin + (int64_t)chunk * chunk_stride;
   const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  if (row0 >= row1) return;
   const int nrows = (int)(row1 - row0);
   const int ntiles = (nrows + RT - 1) / RT;
 
@@ -250,7 +259,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
     // lane (ri, h=0) holds query ri's threshold; slot [m][h'][g] wants query (g&3)+8(g>>2)+4h'.
     // The wave's staging area holds the 64 thresholds until the first hit.
-    const int tl = qok ? tau[q] - pc : -0x40000000;  // padded queries never accept
+    const int tl = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;  // padded queries never accept
     if (h == 0) {
       const int g = (ri & 3) | ((ri >> 3) << 2);     // inverse of (g&3) + 8(g>>2)
       stg[(m * 2 + ((ri >> 2) & 1)) * 16 + g] = tl;
@@ -371,6 +380,16 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
   };
   auto row_pc = [&](int pcv, int lr) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
+  // DENSE: all 16 distances of block (m, n-block) -> dv (row lr of the chunk)
+  auto block_dense = [&](const v16f& a, int m, int pc, int lr) {
+    const int64_t col = (int64_t)chunk * chunk_rows + lr;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int v = pc - 2 * (int)a[g];
+      if (q < nq) dv[(int64_t)q * dv_stride + col] = lr < nrows ? (uint16_t)(v + 1024) : (uint16_t)0xFFFF;
+    }
+  };
 
   // ---- main loop: 32 groups per tile; group gi = (n-block gi>>4, k-step gi&15) runs the two
   // MFMAs of M-blocks 0 and 1 on ONE B fragment (read BAHEAD groups ahead into a ring of 4,
@@ -425,11 +444,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       // point IR-level sinking moves them past the scheduling fences
       asm volatile("" : "+v"(acc[nbk][0]), "+v"(acc[nbk][1]));
       if ((gi & 7) == 5 && !(VRQ_BISECT & 2)) unpack_write(pv, gi >> 3, ubw);
-      if constexpr (gi == 22) {  // async flush, step 1: the stage's first 64 entries
+      if constexpr (gi == 22 && !DENSE) {  // async flush, step 1: the stage's first 64 entries
         lds_read32(fe, stg0 + (uint32_t)(l * 4));
         nfl = nst < 64 ? nst : 64;
       }
-      if constexpr (gi == 26)  // step 2: list positions (idle lanes add 0)
+      if constexpr (gi == 26 && !DENSE)  // step 2: list positions (idle lanes add 0)
         lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 63) * 4), l < nfl ? 1 : 0);
       if (gi == 30 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
       // epilogue of the previous n-block (n-block 1 of tile t-1 during n-block 0, n-block 0 of
@@ -440,7 +459,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
         const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
         const int pc = row_pc(pcr_, lr);
         constexpr int m = j == 3 ? 0 : 1;
-        block_hits(pa_[m], m, pc, 0.5f * (float)pc, (nbk == 0 ? 32 : 64) + ri);
+        if constexpr (DENSE)
+          block_dense(pa_[m], m, pcr_, lr);
+        else
+          block_hits(pa_[m], m, pc, 0.5f * (float)pc, (nbk == 0 ? 32 : 64) + ri);
       }
       VRQ_SCHED_FENCE();
     });
@@ -461,92 +483,98 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const int lr = (ntiles - 1) * RT + 32 + ri;
     const int pc = row_pc(pcvP, lr);
     const float hp = 0.5f * (float)pc;
-    block_hits(acc[1][0], 0, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
-    block_hits(acc[1][1], 1, pc, hp, 96 + ri);
+    if constexpr (DENSE) {
+      block_dense(acc[1][0], 0, pcvP, lr);
+      block_dense(acc[1][1], 1, pcvP, lr);
+    } else {
+      block_hits(acc[1][0], 0, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
+      block_hits(acc[1][1], 1, pc, hp, 96 + ri);
+    }
     if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }
   wait_lgkm0();
   const int q = qbase + l;
-  if (q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
+  if (!DENSE && q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
 }
 
-// Thresholds from the exact prefix lists (sorted top-K of rows [0, prefix) per query):
-//   tau_p(q) = d_(K), the K-th smallest prefix distance (1025 when the prefix holds fewer than K
-//              rows): every suffix row with dist >= tau_p ranks after >= K prefix rows, so the
-//              strict test dist < tau_p is exact (the guaranteed threshold);
-//   tau_s(q) = d_(j) + 1 for the plan's j < K (accept dist <= d_(j)): with iid rows the corpus
-//              holds ~j*n/prefix rows below it, >= K with probability 1 - 1e-6 (plan), and the
-//              check kernel proves it per query; cpre(q) = prefix rows with dist < tau_s.
-// With j >= K the plan uses tau_p alone (tau_s = tau_p, no check).
-__global__ __launch_bounds__(256) void prefix_tau_kernel(const uint64_t* __restrict__ lists, int nl, int K, int j,
-                                                         int32_t* __restrict__ tau_s, int32_t* __restrict__ tau_p,
-                                                         int32_t* __restrict__ cpre, int32_t* __restrict__ qbflag,
-                                                         int nqb) {
-  __shared__ uint32_t hist[1025];
+// Thresholds from the dense sample (S rows spread over the corpus, every distance exact):
+//   tau_p(q) = d_(K) + 1, accept dist <= the K-th smallest sample distance: the sample rows alone
+//              put >= K corpus rows under it, so the candidates always hold the exact top-K
+//              (the guaranteed threshold of the re-run);
+//   tau_s(q) = d_(j) + 1 for the plan's j < K: with iid rows the corpus holds ~j*n/S rows under
+//              it, >= K with probability 1 - 1e-6 (plan); sample_check_kernel proves it per query.
+// One workgroup per query: histogram of the S u16 values v + 1024 (v = dist - pc(q)).
+__global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __restrict__ dv, int64_t S,
+                                                            const uint8_t* __restrict__ queries, int K, int j,
+                                                            int32_t* __restrict__ tau_s, int32_t* __restrict__ tau_p,
+                                                            int32_t* __restrict__ qbflag, int nqb) {
+  constexpr int NB = 2049;
+  __shared__ uint32_t hist[NB + 3];
+  __shared__ int pcq;
   const int qi = blockIdx.x, tid = threadIdx.x;
   if (qi == 0 && qbflag)
     for (int i = tid; i < nqb; i += 256) qbflag[i] = 0;
-  for (int i = tid; i < 1025; i += 256) hist[i] = 0;
+  for (int i = tid; i < NB; i += 256) hist[i] = 0;
+  if (tid == 0) pcq = 0;
   __syncthreads();
-  const uint64_t* Lq = lists + (int64_t)qi * nl * K;
-  for (int i = tid; i < nl * K; i += 256) {
-    const uint64_t key = Lq[i];
-    if (key != KEY_NONE) atomicAdd(&hist[(uint32_t)(key >> KEY_ROW_BITS)], 1u);
+  if (tid < 32) atomicAdd(&pcq, __popc(reinterpret_cast<const uint32_t*>(queries + (int64_t)qi * 128)[tid]));
+  const uint16_t* d = dv + (int64_t)qi * S;
+  const int64_t S8 = S & ~int64_t(7);
+  for (int64_t i = (int64_t)tid * 8; i < S8; i += 256 * 8) {  // 16-B loads: 8 values
+    const uint4 w = *reinterpret_cast<const uint4*>(d + i);
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = x[k] & 0xffff, hi = x[k] >> 16;
+      if (lo < NB) atomicAdd(&hist[lo], 1u);
+      if (hi < NB) atomicAdd(&hist[hi], 1u);
+    }
   }
+  for (int64_t i = S8 + tid; i < S; i += 256)
+    if (d[i] < NB) atomicAdd(&hist[d[i]], 1u);
   __syncthreads();
-  if (tid < 64) {  // one wave: prefix sums over 1025 bins, 17 per lane
+  if (tid < 64) {  // one wave: prefix sums over NB bins, 33 per lane
+    constexpr int BPL = (NB + 63) / 64;
     int loc = 0;
-    for (int i = 0; i < 17; ++i) {
-      const int d = tid * 17 + i;
-      if (d < 1025) loc += (int)hist[d];
+    for (int i = 0; i < BPL; ++i) {
+      const int b = tid * BPL + i;
+      if (b < NB) loc += (int)hist[b];
     }
     int inc = loc;
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(inc, o, 64);
       if (tid >= o) inc += y;
     }
-    // K-th and j-th smallest: bin d holds them iff cum < k <= cum + hist[d]
-    int cum = inc - loc, rk = 1025, rj = 1025, cj = 0x7fffffff;
-    for (int i = 0; i < 17; ++i) {
-      const int d = tid * 17 + i;
-      if (d < 1025) {
-        const int hh = (int)hist[d];
-        if (cum < K && cum + hh >= K) rk = d;
-        if (cum < j && cum + hh >= j) {
-          rj = d;
-          cj = cum + hh;  // rows with dist <= d_(j)
-        }
+    // k-th smallest: bin b holds it iff cum < k <= cum + hist[b]
+    int cum = inc - loc, rk = NB, rj = NB;
+    for (int i = 0; i < BPL; ++i) {
+      const int b = tid * BPL + i;
+      if (b < NB) {
+        const int hh = (int)hist[b];
+        if (cum < K && cum + hh >= K) rk = b;
+        if (cum < j && cum + hh >= j) rj = b;
         cum += hh;
       }
     }
-    // exactly one lane (or none) found each
     for (int o = 32; o > 0; o >>= 1) {
       rk = min(rk, __shfl_xor(rk, o, 64));
       rj = min(rj, __shfl_xor(rj, o, 64));
-      cj = min(cj, __shfl_xor(cj, o, 64));
     }
     if (tid == 0) {
-      const int total = __shfl(inc, 63, 64);
-      tau_p[qi] = rk;
-      if (j >= K) {
-        tau_s[qi] = rk;
-      } else if (rj < 1025) {
-        tau_s[qi] = rj + 1;
-        cpre[qi] = cj;
-      } else {  // fewer than j prefix rows: accept everything
-        tau_s[qi] = 1025;
-        cpre[qi] = total;
-      }
+      // fewer than K valid sample values (not for a planned sample): accept every row
+      const int dk = rk < NB ? rk - 1024 + pcq : 1024;
+      const int dj = rj < NB ? rj - 1024 + pcq : 1024;
+      tau_p[qi] = dk + 1;
+      tau_s[qi] = (j < K ? dj : dk) + 1;
     }
   }
 }
 
-// Proof of the sampled threshold per query: C = cpre + suffix rows with dist < tau_s (the list
-// lengths; an overflowed list counts > capc, and its exact rescan needs no threshold).  C >= K
-// means the K-th smallest key of the whole corpus has dist < tau_s, so the candidates hold the
+// Proof of the sampled threshold per query: C = candidates with dist < tau_s over the whole corpus
+// (the list lengths; an overflowed list counts > capc, and its exact rescan needs no threshold).
+// C >= K means the K-th smallest key of the corpus has dist < tau_s, so the candidates hold the
 // exact top-K.  Otherwise the query is flagged for the re-run with tau_p.  One wave per query.
-__global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __restrict__ cpre,
-                                                           const int32_t* __restrict__ ccnt, int nchunks, int K,
+__global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __restrict__ ccnt, int nchunks, int K,
                                                            int nq, int32_t* __restrict__ rerun,
                                                            int32_t* __restrict__ qbflag) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
@@ -554,7 +582,7 @@ __global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __rest
   int64_t c = 0;
   for (int i = l; i < nchunks; i += 64) c += ccnt[(int64_t)q * nchunks + i];
   c = wave_sum_i64(c);
-  const bool fail = cpre[q] + c < K;
+  const bool fail = c < K;
   if (l == 0) {
     rerun[q] = fail ? 1 : 0;
     if (fail) atomicOr(&qbflag[q / QPB], 1);
@@ -780,42 +808,50 @@ static int sample_order(double lam, int K) {
 
 int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   if (nq < 1 || K < 1 || K > kMfmaMaxK) return VRQ_EUNSUPPORTED;
-  int64_t S = n / kMfmaPrefixDiv;
-  if (S < kMfmaMinPrefix) S = kMfmaMinPrefix;
-  if (S > n) S = n;
-  p->prefix = S;
   p->nqb = (nq + QPB - 1) / QPB;
-  const int64_t rest = n - S;
-  int64_t want = 256 / p->nqb;  // one workgroup per CU
+  // sample: nsc chunks of RT-aligned rows spread evenly over [0, n), S rows in total.
+  // VRQ_SAMPLE_DIV: tuning override of the sample fraction (read per call, no state)
+  const char* ev = getenv("VRQ_SAMPLE_DIV");
+  const int64_t div = ev && atoi(ev) >= 2 ? atoi(ev) : kMfmaSampleDiv;
+  int64_t S = n / div;
+  if (S < kMfmaMinSample) S = kMfmaMinSample;
+  if (S > n) S = n;
+  int64_t nsc = 256 / p->nqb;  // one workgroup per CU
+  if (nsc < 1) nsc = 1;
+  int64_t scr = ((S + nsc - 1) / nsc + RT - 1) / RT * RT;
+  nsc = (S + scr - 1) / scr;
+  p->sample_chunk_rows = scr;
+  p->sample_chunks = (int)nsc;
+  p->sample_stride = n / nsc;  // >= scr since S <= n
+  p->sample = nsc * scr;       // dv columns (rows past n are marked invalid)
+  // thresholded pass over all n rows
+  int64_t want = 256 / p->nqb;
   if (want < 1) want = 1;
-  int64_t cr = (rest + want - 1) / want;
+  int64_t cr = (n + want - 1) / want;
   cr = (cr + RT - 1) / RT * RT;
   if (cr < RT) cr = RT;
   p->chunk_rows = cr;
-  p->nchunks = rest > 0 ? (int)((rest + cr - 1) / cr) : 0;
-  // per-(query, chunk) list capacity: 4x the expected hits K * chunk_rows / prefix (iid rows)
+  p->nchunks = (int)((n + cr - 1) / cr);
+  // per-(query, chunk) list capacity: 4x the hits expected under tau_p (K * cr / S, iid rows)
   const int64_t expect = (K * cr + S - 1) / S;
   int capc = 64;
   while (capc < 4 * expect && capc < 4096) capc <<= 1;
   p->capc = capc;
   p->j = sample_order((double)K * (double)S / (double)n, K);
-  if (scan_plan(S, 128, nq, K, &p->prefix_plan) != VRQ_OK) return VRQ_EUNSUPPORTED;
-  if (p->prefix_plan.nchunks + 1 > 4096) return VRQ_EUNSUPPORTED;  // select step's list bound
-  p->nl = p->prefix_plan.nchunks + 1;  // prefix chunk lists + the suffix list
-  // workspace: prefix lists [nq][nlp][K] | suffix list [nq][K] | cand [nq][nchunks][capc] |
-  //            list lengths [nq][nchunks] | tau_s, tau_p, cpre, rerun [nq] | qbflag [nqb]
+  // workspace: dv [nq][sample] u16 | suffix list [nq][K] | cand [nq][nchunks][capc] |
+  //            list lengths [nq][nchunks] | tau_s, tau_p, rerun [nq] | qbflag [nqb]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  p->off_suffix = al(p->prefix_plan.list_bytes);
+  p->off_suffix = al((size_t)nq * p->sample * sizeof(uint16_t));
   p->off_cand = p->off_suffix + al((size_t)nq * K * sizeof(uint64_t));
   p->off_cnt = p->off_cand + al((size_t)nq * p->nchunks * p->capc * sizeof(uint64_t));
   p->off_tau = p->off_cnt + al((size_t)nq * p->nchunks * sizeof(int32_t));
-  p->bytes = p->off_tau + 4 * al((size_t)nq * sizeof(int32_t)) + (size_t)p->nqb * sizeof(int32_t);
+  p->bytes = p->off_tau + 3 * al((size_t)nq * sizeof(int32_t)) + (size_t)p->nqb * sizeof(int32_t);
   return VRQ_OK;
 }
 
 bool mfma_use(int64_t n, int nq, int K, int flags) {
   if (flags & VRQ_SEARCH_SCAN_VALU) return false;
-  const bool ok = K <= kMfmaMaxK && n >= 2 * kMfmaMinPrefix;
+  const bool ok = K <= kMfmaMaxK && n >= kMfmaMinRows;
   if (flags & VRQ_SEARCH_SCAN_MFMA) return ok;
   return ok && nq >= kMfmaMinQueries;
 }
@@ -824,42 +860,45 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                      uint8_t* ws, hipStream_t s, int flags) {
   constexpr int ALL = VRQ_SCAN_STAGE_PREFIX | VRQ_SCAN_STAGE_MATRIX | VRQ_SCAN_STAGE_SUFFIX;
   const int st = (flags & ALL) ? (flags & ALL) : ALL;
-  uint64_t* lists = (uint64_t*)ws;
+  uint16_t* dv = (uint16_t*)ws;
   uint64_t* suffix = (uint64_t*)(ws + p.off_suffix);
   uint64_t* cand = (uint64_t*)(ws + p.off_cand);
   int32_t* ccnt = (int32_t*)(ws + p.off_cnt);
   const size_t qa = ((size_t)nq * sizeof(int32_t) + 255) & ~size_t(255);
   int32_t* tau_s = (int32_t*)(ws + p.off_tau);
   int32_t* tau_p = (int32_t*)(ws + p.off_tau + qa);
-  int32_t* cpre = (int32_t*)(ws + p.off_tau + 2 * qa);
-  int32_t* rerun = (int32_t*)(ws + p.off_tau + 3 * qa);
-  int32_t* qbflag = (int32_t*)(ws + p.off_tau + 4 * qa);
+  int32_t* rerun = (int32_t*)(ws + p.off_tau + 2 * qa);
+  int32_t* qbflag = (int32_t*)(ws + p.off_tau + 3 * qa);
   const bool sampled = p.j < K;
-  if (st & VRQ_SCAN_STAGE_PREFIX) {
-    int rc = scan_launch(p.prefix_plan, codes, p.prefix, 128, q, nq, K, lists, s);
-    if (rc != VRQ_OK) return rc;
-    hipLaunchKernelGGL(prefix_tau_kernel, dim3(nq), dim3(256), 0, s, lists, p.prefix_plan.nchunks, K, p.j, tau_s,
-                       tau_p, cpre, qbflag, p.nqb);
+  const int32_t* none = nullptr;
+  if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
+    hipLaunchKernelGGL(hamming_mfma_kernel<true>, dim3(p.sample_chunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+                       (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0, p.sample_chunk_rows,
+                       p.sample_stride, p.sample_chunks, p.nqb, none, none, dv, p.sample);
+    VRQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
+                       tau_s, tau_p, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
-  if ((st & VRQ_SCAN_STAGE_MATRIX) && p.nchunks > 0) {
-    hipLaunchKernelGGL(hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n, p.prefix,
-                       q, nq, tau_s, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb, (const int32_t*)nullptr,
-                       (const int32_t*)nullptr);
+  if (st & VRQ_SCAN_STAGE_MATRIX) {
+    hipLaunchKernelGGL(hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+                       (int64_t)0, q, nq, (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.capc,
+                       p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb, none, none, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
     if (sampled) {
       // prove C >= K per query; re-run the query blocks holding a failed query with tau_p
-      hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, cpre, ccnt, p.nchunks, K, nq,
-                         rerun, qbflag);
+      hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, (const int32_t*)ccnt, p.nchunks,
+                         K, nq, rerun, qbflag);
       VRQ_LAUNCH_CHECK();
-      hipLaunchKernelGGL(hamming_mfma_kernel, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
-                         p.prefix, q, nq, tau_p, cand, ccnt, p.capc, p.chunk_rows, p.nchunks, p.nqb,
-                         (const int32_t*)rerun, (const int32_t*)qbflag);
+      hipLaunchKernelGGL(hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+                         (int64_t)0, q, nq, (const int32_t*)tau_p, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows,
+                         p.nchunks, p.nqb, (const int32_t*)rerun, (const int32_t*)qbflag, (uint16_t*)nullptr,
+                         (int64_t)0);
       VRQ_LAUNCH_CHECK();
     }
   }
-  if (st & VRQ_SCAN_STAGE_SUFFIX) {
-    hipLaunchKernelGGL(suffix_topk_kernel, dim3(nq), dim3(SUF_THREADS), 0, s, codes, n, p.prefix, q, cand, ccnt,
+  if (st & VRQ_SCAN_STAGE_SUFFIX) {  // candidates of the whole corpus -> one sorted K-list per query
+    hipLaunchKernelGGL(suffix_topk_kernel, dim3(nq), dim3(SUF_THREADS), 0, s, codes, n, (int64_t)0, q, cand, ccnt,
                        p.nchunks, p.capc, K, suffix);
     VRQ_LAUNCH_CHECK();
   }

@@ -511,7 +511,7 @@ size_t vrq_search3_workspace_size(int64_t n, int32_t dim, int32_t nq, int32_t K)
   ScanPlan p;
   if (scan_plan(n, dim / 8, nq, K, &p) != VRQ_OK) return 0;
   MfmaPlan mp;
-  if (K <= kMfmaMaxK && n >= 2 * kMfmaMinPrefix && mfma_plan(n, nq, K, &mp) == VRQ_OK)
+  if (K <= kMfmaMaxK && n >= kMfmaMinRows && mfma_plan(n, nq, K, &mp) == VRQ_OK)
     return mp.bytes > p.list_bytes ? mp.bytes : p.list_bytes;
   return p.list_bytes;
 }
@@ -560,9 +560,8 @@ int vrq_hamming_topk(const uint8_t* codes, int64_t n, int32_t code_bytes, int64_
     if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
     rc = mfma_scan_launch(mp, codes, n, queries, nq, k, (uint8_t*)workspace, s, 0);
     if (rc != VRQ_OK) return rc;
-    return launch_select(s, nq, lists, mp.prefix_plan.nchunks,
-                         (const uint64_t*)((uint8_t*)workspace + mp.off_suffix), k, nullptr, nullptr, nullptr,
-                         nullptr, 1, fa);
+    return launch_select(s, nq, lists, 0, (const uint64_t*)((uint8_t*)workspace + mp.off_suffix), k, nullptr,
+                         nullptr, nullptr, nullptr, 1, fa);
   }
   ScanPlan p;
   int rc = scan_plan(n, code_bytes, nq, k, &p);
@@ -621,7 +620,7 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
     const int rc = mfma_plan(n, nq, K, &mp);
     if (rc != VRQ_OK) return rc;
     if (workspace_bytes < mp.bytes) return VRQ_EWORKSPACE;
-    nlp = mp.prefix_plan.nchunks;
+    nlp = 0;  // the matrix-core scan leaves one sorted list per query
     suffix = (const uint64_t*)((const uint8_t*)workspace + mp.off_suffix);
   } else {
     ScanPlan p;
@@ -668,7 +667,7 @@ int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, 
     MfmaPlan mp;
     const int rc = mfma_plan(n, nq, K, &mp);
     if (rc != VRQ_OK) return rc;
-    if (prefix_rows) *prefix_rows = mp.prefix;
+    if (prefix_rows) *prefix_rows = 0;  // every row goes through the matrix-core pass
     return VRQ_SCAN_KIND_MFMA;
   }
   ScanPlan p;

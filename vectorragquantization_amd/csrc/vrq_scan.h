@@ -31,20 +31,22 @@ int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, cons
                 uint64_t* lists, hipStream_t s);
 
 // ---- K1m: matrix-core scan for large query batches (hamming_mfma.hip) ----
-constexpr int kMfmaMaxK = 128;           // K bound of the path (expected suffix candidates ~15 K per query)
-constexpr int64_t kMfmaMinPrefix = 32768;
+constexpr int kMfmaMaxK = 128;           // K bound of the path
+constexpr int64_t kMfmaMinSample = 32768;
+constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
 constexpr int kMfmaMinQueries = 128;     // auto-selection threshold on the batch size
-constexpr int64_t kMfmaPrefixDiv = 16;   // exact prefix = n / kMfmaPrefixDiv rows
+constexpr int64_t kMfmaSampleDiv = 32;   // dense threshold sample = n / kMfmaSampleDiv rows
 
 struct MfmaPlan {
-  int64_t prefix;      // rows [0, prefix) scanned exactly by K1 -> tau(q)
-  int capc;            // candidate capacity per (query, chunk) list
-  int j;               // sampled threshold order (tau_s = d_(j) + 1 of the prefix); K = tau_p only
-  int nqb;             // 256-query blocks
-  int64_t chunk_rows;  // suffix rows per workgroup (multiple of 64)
+  int64_t sample;            // dense sample columns (sample_chunks * sample_chunk_rows)
+  int64_t sample_chunk_rows;
+  int64_t sample_stride;     // sample chunk c starts at row c * sample_stride
+  int sample_chunks;
+  int j;                     // sampled threshold order (tau_s = d_(j) + 1); K = tau_p only
+  int capc;                  // candidate capacity per (query, chunk) list
+  int nqb;                   // 256-query blocks
+  int64_t chunk_rows;        // rows per workgroup of the thresholded pass (multiple of 64)
   int nchunks;
-  int nl;              // lists handed to the select step: prefix chunk lists + 1 suffix list
-  ScanPlan prefix_plan;
   size_t off_suffix, off_cand, off_cnt, off_tau, bytes;
 };
 
