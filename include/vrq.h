@@ -49,13 +49,14 @@ extern "C" {
 #define VRQ_SEARCH_SCAN_MFMA 8   /* Phase-I scan: force the matrix-core scan wherever it is
                                     supported (K <= 128, n >= 65536); by default it is used for
                                     nq >= 128.  Both scans give identical results. */
-/* vrq_search3_scan only, matrix-core scan only: run a subset of its three stages (none set =
- * all), so a caller can bracket each stage with events; issuing the three in order on one
- * stream is exactly the full scan. */
+/* vrq_search3_scan only, matrix-core scan only: run a subset of its four stages (none set =
+ * all), so a caller can bracket each stage with events; issuing PREFIX, MATRIX, RECHECK,
+ * SUFFIX in that order on one stream is exactly the full scan. */
 #define VRQ_SCAN_STAGE_PREFIX 16 /* dense matrix-core pass over a spread row sample -> per-query
                                     thresholds (sampled d_(j), guaranteed d_(K)) */
-#define VRQ_SCAN_STAGE_MATRIX 32 /* thresholded matrix-core pass over all rows (+ per-query proof
-                                    and exact re-run of the rare failed query blocks) */
+#define VRQ_SCAN_STAGE_MATRIX 32 /* thresholded matrix-core pass over all rows */
+#define VRQ_SCAN_STAGE_RECHECK 128 /* per-query proof that the sampled threshold admitted >= K rows
+                                      and exact re-run of the rare failed query blocks */
 #define VRQ_SCAN_STAGE_SUFFIX 64 /* candidates -> one sorted K-list per query (exact rescan on
                                     list overflow) */
 

@@ -132,7 +132,8 @@ def test_mfma_stage_split_equals_full_scan(dev, oracle_lib):
     rows = torch.empty((nq, K), dtype=torch.int64, device=dev)
     dist = torch.empty((nq, K), dtype=torch.int32, device=dev)
     base = N.VRQ_SEARCH_PHASE1_ONLY | N.VRQ_SEARCH_SCAN_MFMA
-    for stage in (N.VRQ_SCAN_STAGE_PREFIX, N.VRQ_SCAN_STAGE_MATRIX, N.VRQ_SCAN_STAGE_SUFFIX):
+    for stage in (N.VRQ_SCAN_STAGE_PREFIX, N.VRQ_SCAN_STAGE_MATRIX, N.VRQ_SCAN_STAGE_RECHECK,
+                  N.VRQ_SCAN_STAGE_SUFFIX):
         N.check(lib.vrq_search3_scan(N.ptr(c_t), n, 1024, N.ptr(q_t), nq, K, base | stage, N.ptr(ws), ws.numel(),
                                      st), "scan stage")
     N.check(lib.vrq_search3_finish(N.ptr(c_t), None, None, None, n, 1024, 0, None, nq, K, K, K, base, N.ptr(cnt),

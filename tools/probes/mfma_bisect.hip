@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
   float best = 1e30f;
   for (int it = 0; it < 6; ++it) {
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(vrq::hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes,
+    hipLaunchKernelGGL(vrq::hamming_mfma_kernel<vrq::MFMA_MAIN>, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes,
                        n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
     (void)hipEventRecord(e1, 0);

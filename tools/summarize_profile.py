@@ -12,8 +12,13 @@ import sys
 
 
 def short(name):
-    if "hamming_mfma" in name:
-        return "hamming_mfma_kernel"
+    if "hamming_mfma" in name:  # template MODE: 0 thresholded pass, 1 dense sample pass, 2 re-run
+        return {"1": "hamming_mfma_kernel_sample", "2": "hamming_mfma_kernel_rerun"}.get(
+            name.split("hamming_mfma_kernel<", 1)[-1][:1], "hamming_mfma_kernel")
+    if "sample_select" in name:
+        return "sample_select_kernel"
+    if "sample_check" in name:
+        return "sample_check_kernel"
     if "prefix_tau" in name:
         return "prefix_tau_kernel"
     if "suffix_topk" in name:

@@ -25,6 +25,7 @@ VRQ_SEARCH_SCAN_MFMA = 8
 VRQ_SCAN_STAGE_PREFIX = 16
 VRQ_SCAN_STAGE_MATRIX = 32
 VRQ_SCAN_STAGE_SUFFIX = 64
+VRQ_SCAN_STAGE_RECHECK = 128
 VRQ_SCAN_KIND_VALU = 0
 VRQ_SCAN_KIND_MFMA = 1
 

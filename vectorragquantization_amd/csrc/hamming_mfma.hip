@@ -164,12 +164,17 @@ constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
 // as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + row].  Chunk c covers
 // rows [row_begin + c * chunk_stride, + chunk_rows) (the sample spreads its chunks over the corpus;
 // the thresholded pass uses chunk_stride = chunk_rows).
-template <bool DENSE>
+// MODE: MFMA_MAIN (thresholded pass), MFMA_SAMPLE (dense sample pass, DENSE below) or MFMA_RERUN
+// (the exact re-run of failed query blocks: same code as MAIN, a separate symbol so profiles and
+// traces tell the two launches apart).
+enum { MFMA_MAIN = 0, MFMA_SAMPLE = 1, MFMA_RERUN = 2 };
+template <int MODE>
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
+  constexpr bool DENSE = MODE == MFMA_SAMPLE;
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM_BYTES];
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
@@ -858,7 +863,7 @@ bool mfma_use(int64_t n, int nq, int K, int flags) {
 
 int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
                      uint8_t* ws, hipStream_t s, int flags) {
-  constexpr int ALL = VRQ_SCAN_STAGE_PREFIX | VRQ_SCAN_STAGE_MATRIX | VRQ_SCAN_STAGE_SUFFIX;
+  constexpr int ALL = VRQ_SCAN_STAGE_PREFIX | VRQ_SCAN_STAGE_MATRIX | VRQ_SCAN_STAGE_RECHECK | VRQ_SCAN_STAGE_SUFFIX;
   const int st = (flags & ALL) ? (flags & ALL) : ALL;
   uint16_t* dv = (uint16_t*)ws;
   uint64_t* suffix = (uint64_t*)(ws + p.off_suffix);
@@ -872,7 +877,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   const bool sampled = p.j < K;
   const int32_t* none = nullptr;
   if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
-    hipLaunchKernelGGL(hamming_mfma_kernel<true>, dim3(p.sample_chunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_SAMPLE>, dim3(p.sample_chunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
                        (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0, p.sample_chunk_rows,
                        p.sample_stride, p.sample_chunks, p.nqb, none, none, dv, p.sample);
     VRQ_LAUNCH_CHECK();
@@ -881,21 +886,21 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_SCAN_STAGE_MATRIX) {
-    hipLaunchKernelGGL(hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_MAIN>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
                        (int64_t)0, q, nq, (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.capc,
                        p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb, none, none, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
-    if (sampled) {
-      // prove C >= K per query; re-run the query blocks holding a failed query with tau_p
-      hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, (const int32_t*)ccnt, p.nchunks,
-                         K, nq, rerun, qbflag);
-      VRQ_LAUNCH_CHECK();
-      hipLaunchKernelGGL(hamming_mfma_kernel<false>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
-                         (int64_t)0, q, nq, (const int32_t*)tau_p, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows,
-                         p.nchunks, p.nqb, (const int32_t*)rerun, (const int32_t*)qbflag, (uint16_t*)nullptr,
-                         (int64_t)0);
-      VRQ_LAUNCH_CHECK();
-    }
+  }
+  if ((st & VRQ_SCAN_STAGE_RECHECK) && sampled) {
+    // prove C >= K per query; re-run the query blocks holding a failed query with tau_p
+    hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, (const int32_t*)ccnt, p.nchunks, K,
+                       nq, rerun, qbflag);
+    VRQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_RERUN>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
+                       (int64_t)0, q, nq, (const int32_t*)tau_p, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows,
+                       p.nchunks, p.nqb, (const int32_t*)rerun, (const int32_t*)qbflag, (uint16_t*)nullptr,
+                       (int64_t)0);
+    VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_SCAN_STAGE_SUFFIX) {  // candidates of the whole corpus -> one sorted K-list per query
     hipLaunchKernelGGL(suffix_topk_kernel, dim3(nq), dim3(SUF_THREADS), 0, s, codes, n, (int64_t)0, q, cand, ccnt,
