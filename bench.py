@@ -16,6 +16,10 @@ same query batch per step for every N); results are identical for every N.
 
 --config c3 runs the Phase-I-only HBM-roofline case instead (uniform random
 codes, queries = corpus rows with 64-256 flipped bits).
+--config c5 runs BASELINE config 5: the batched Phase-II + Phase-III scoring of
+nq = 1024 queries against EVERY row of a 10M x 1024 corpus on the matrix cores
+(vrq_gemm_topk, int8-split queries x int8 / 0-1 rows on v_mfma_i32_32x32x32_i8),
+top-k fused; one step = both phases for the batch.
 
 rank 0 prints ONE JSON line (see README of the driver contract).
 """
@@ -56,7 +60,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2")
     ap.add_argument("--n", type=int, default=None, help="corpus rows (total over all ranks)")
     ap.add_argument("--nq", type=int, default=None, help="queries per step")
     ap.add_argument("--k", type=int, default=10)
@@ -286,6 +290,155 @@ def measured_mfma_peak():
         return None
 
 
+I8_DENSE_PEAK_TOPS = 1024 * 2048 * 2.4e9 / 1e12  # v_mfma_i32_32x32x32_i8: 32 cycles, 2x the bf16 rate
+
+
+class C5Pipeline:
+    """Config 5 step: vrq_gemm_topk(BINARY) then vrq_gemm_topk(INT8_COSINE) over the shard, each as its
+    three stages (sample / main / finish) bracketed by HIP events on the library's stream; N > 1: one
+    all-gather of both phases' [nq, k] results + the (score desc, row asc) merge."""
+
+    def __init__(self, codes, x8, norms, row0, qf, k, world):
+        self.lib = N.load()
+        self.codes, self.x8, self.norms, self.row0, self.qf, self.k, self.world = codes, x8, norms, row0, qf, k, world
+        dev = codes.device
+        nq, m = qf.shape[0], codes.shape[0]
+        ws = max(self.lib.vrq_gemm_topk_workspace_size(mo, m, 1024, nq, k) for mo in (2, 3))
+        assert ws > 0, "unsupported config-5 shape"
+        self.ws = torch.empty((ws,), dtype=torch.uint8, device=dev)
+        self.out = {mo: (torch.empty((nq,), dtype=torch.int32, device=dev),
+                         torch.empty((nq, k), dtype=torch.int64, device=dev),
+                         torch.empty((nq, k), dtype=torch.float64, device=dev)) for mo in (2, 3)}
+        self.ev, self.final = [], None
+
+    def _call(self, mode, stage, st):
+        c, r, s = self.out[mode]
+        N.check(self.lib.vrq_gemm_topk(mode, N.ptr(self.codes), N.ptr(self.x8), N.ptr(self.norms),
+                                       self.codes.shape[0], 1024, self.row0, N.ptr(self.qf), self.qf.shape[0],
+                                       self.k, stage, N.ptr(c), N.ptr(r), N.ptr(s), N.ptr(self.ws), self.ws.numel(),
+                                       st), "vrq_gemm_topk")
+
+    def step(self, record):
+        st = N.stream_handle(self.codes.device)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if record else None
+        rec = (lambda i: e[i].record()) if record else (lambda i: None)
+        i = 0
+        rec(i)
+        for mode in (N.VRQ_GEMM_BINARY, N.VRQ_GEMM_INT8_COSINE):
+            for stage in (N.VRQ_GEMM_STAGE_SAMPLE, N.VRQ_GEMM_STAGE_MAIN, N.VRQ_GEMM_STAGE_FINISH):
+                self._call(mode, stage, st)
+                i += 1
+                rec(i)
+        if self.world > 1:
+            from vectorragquantization_amd.dist import gather_topk, merge_topk_shards
+            self.final = {}
+            for mode in (2, 3):
+                gr, gs = gather_topk(self.out[mode][1], self.out[mode][2])
+                self.final[mode] = merge_topk_shards(gr, gs, self.k)
+        else:
+            self.final = self.out
+        rec(7)
+        if record:
+            self.ev.append(e)
+
+    def stage_ms(self):
+        def mean(i, j):
+            return float(np.mean([ev[i].elapsed_time(ev[j]) for ev in self.ev]))
+        names = ["binary_sample", "binary_main", "binary_finish", "cosine_sample", "cosine_main", "cosine_finish"]
+        d = {nm: mean(j, j + 1) for j, nm in enumerate(names)}
+        d["collective"] = mean(6, 7)
+        return d
+
+
+def cpu_baseline_c5(codes_h, x8_h, qf_h, k, n, nq_s=4, threads=16):
+    """Reference arithmetic on the host (NumPy): Phase-II float64 GEMV over 2*unpackbits-1 and Phase-III
+    float32 dot / float64 norm for every row, stable desc top-k -- on nq_s queries x the given leading
+    rows, scaled to queries/s over the n-row corpus."""
+    from oracle import oracle_np as O
+    rs = codes_h.shape[0]
+    t0 = time.perf_counter()
+    for q in range(nq_s):
+        for mode in ("binary", "int8_cosine"):
+            S = np.concatenate([O.exhaustive_scores(mode, qf_h[q:q + 1], codes=codes_h[a:a + 65536],
+                                                    x8=x8_h[a:a + 65536]) for a in range(0, rs, 65536)], 1)
+            O.exhaustive_topk(S, k)
+    t = time.perf_counter() - t0
+    return {"value": nq_s / (t * n / rs), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{nq_s} queries x the first {rs} of {n} rows, both phases (NumPy float64 GEMV over "
+                      f"2*unpackbits-1; float32 dot / float64 norm), {t:.1f} s, scaled by n/{rs}"}
+
+
+def run_c5(a, world, rank, dev):
+    n = a.n or 10_000_000
+    nq = a.nq or 1024
+    t_setup = time.perf_counter()
+    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+    codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
+    qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] c5 data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
+    P = C5Pipeline(codes, x8, norms, row0, qf, a.k, world)
+    for _ in range(a.warmup):
+        P.step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        P.step(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    T = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([T], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        T = float(tt.item())
+    rec = None
+    if not a.no_recall:
+        rec = recall_at_10(P.final[3][1], qf, n, rank, world, dev, min(a.recall_sample, nq))
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    st = P.stage_ms()
+    m = codes.shape[0]
+    ops = 2.0 * nq * m * 1024  # algorithmic MACs x 2 per phase
+    tag = f"c5_n{n}_nq{nq}_g{world}"
+    roof = {"bound": "mfma", "achieved": ops / (st["cosine_main"] * 1e-3) / 1e12, "peak": I8_DENSE_PEAK_TOPS / 2,
+            "unit": "TOPS", "kernel": "gemm_topk_kernel<INT8_COSINE> main pass (v_mfma_i32_32x32x32_i8, 2 query "
+            "pieces)", "kernel_ms": st["cosine_main"], "algorithmic_ops_per_launch": ops,
+            "peak_note": "i8 dense peak / 2 (two int8 pieces per query = the algorithmic ceiling; equals the "
+                         "bf16 dense peak SURVEY.md 8(d) prices config 5 against)",
+            "mfma_issue_frac_i8": 2 * ops / (st["cosine_main"] * 1e-3) / 1e12 / I8_DENSE_PEAK_TOPS,
+            "algorithmic_bytes_per_launch": m * 1024 + m * 8, "traffic": pmc_traffic(tag, "gemm_topk_kernel")}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof_bin = {"achieved": ops / (st["binary_main"] * 1e-3) / 1e12, "kernel_ms": st["binary_main"],
+                "kernel": "gemm_topk_kernel<BINARY> main pass", "algorithmic_bytes_per_launch": m * 128}
+    roof_bin["frac"] = roof_bin["achieved"] / roof["peak"]
+    out = {
+        "metric": METRIC, "value": nq * a.steps / T, "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "i8 (int8-split f32 queries) + f64 rescoring",
+        "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)",
+        "config": {"workload": f"BASELINE config 5: batched Phase-II + Phase-III exhaustive scoring, {n} x 1024 "
+                               f"corpus, nq={nq} queries per step, fused top-{a.k}",
+                   "corpus_rows": n, "nq": nq, "k": a.k,
+                   "parallelism": f"row-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU"},
+        "recall_at_10": rec, "phase_ms": st, "roofline": roof, "roofline_binary": roof_bin,
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        rs = min(m, 1_000_000)
+        out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
+                                              a.k, m, threads=a.cpu_threads)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,6 +449,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+    if a.config == "c5":
+        return run_c5(a, world, rank, dev)
     phase1 = a.config == "c3"
     n = a.n or (100_000_000 if phase1 else 1_000_000)
     nq = a.nq or (8 if phase1 else 1024)

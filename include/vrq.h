@@ -181,6 +181,32 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
 
 /* np.linalg.norm(int8 row) in float64 (CohereEnhancedVectorDB.py:308), computed once at add time */
 int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, void* stream);
+/* ---------------------------------------------------------------------------
+ * Exhaustive batched Phase-II / Phase-III scoring on the matrix cores (BASELINE config 5):
+ * the per-candidate scores of CohereEnhancedVectorDB.py:283-293 (VRQ_GEMM_BINARY) or :302-318
+ * (VRQ_GEMM_INT8_COSINE) evaluated against EVERY row, top-k fused (no nq x n score matrix):
+ *   VRQ_GEMM_BINARY       s = float(q . (2*unpackbits(code)-1)) in float64      (codes)
+ *   VRQ_GEMM_INT8_COSINE  s = float32(q . int8) / ||int8||_2, -inf if the norm is 0 (x8, norms)
+ * out_rows i64[nq, k] / out_scores f64[nq, k]: the k rows with the largest s ordered (s desc,
+ * row asc) -- the reference's stable sorted(..., reverse=True) (:296, :321) over rows in index
+ * order -- as row_offset + row, with their exact scores (bit-identical to vrq_search3's);
+ * out_count i32[nq] = min(k, n); unused slots -1 / NaN.  Queries must be finite.
+ * Exact for every input: int8-split queries on v_mfma_i32_32x32x32_i8 give scores within a
+ * proven per-query bound, a sampled threshold keeps every row that can reach the top-k, and the
+ * survivors are rescored exactly (heavy-tie inputs fall back to an exact scan of every row).
+ * flags: 0, or a subset of the VRQ_GEMM_STAGE_* (issued in order = the full call).
+ * Supported: dim = 1024, 1 <= k <= 1024, 1 <= n < 2^32.
+ * ------------------------------------------------------------------------- */
+#define VRQ_GEMM_BINARY 2
+#define VRQ_GEMM_INT8_COSINE 3
+#define VRQ_GEMM_STAGE_SAMPLE 16 /* query split + dense sample pass + per-query thresholds */
+#define VRQ_GEMM_STAGE_MAIN 32   /* thresholded pass over every row -> candidate lists */
+#define VRQ_GEMM_STAGE_FINISH 64 /* exact rescoring + sort of the candidates (+ exact fallback) */
+size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k);
+int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
+                  int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
+                  int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,
+                  size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

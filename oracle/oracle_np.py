@@ -204,6 +204,39 @@ def three_phase_batch(codes: np.ndarray, int8: np.ndarray, ids: np.ndarray,
     return out
 
 
+def exhaustive_scores(mode: str, qf: np.ndarray, codes: np.ndarray = None, x8: np.ndarray = None) -> np.ndarray:
+    """Reference Phase-II or Phase-III score of EVERY row for each query (config 5), f64 [nq, n].
+
+    ``"binary"``: ``float(q . (2*unpackbits(code)-1))`` with the float32 query promoted to float64
+    (``CohereEnhancedVectorDB.py:283-293``; every product is +-q_i, so the float64 GEMV equals the
+    reference's per-candidate ddot).  ``"int8_cosine"``: ``float32(q . int8) / ||int8||``, -inf for
+    a zero norm (``:302-318``), with the float32 dot taken as the correctly rounded exact dot (the
+    GPU's definition; NumPy's sdot is within a few ulps of it).
+    """
+    q64 = np.asarray(qf, dtype=np.float32).astype(np.float64)
+    if mode == "binary":
+        pm = (2 * np.unpackbits(codes, axis=1).astype(np.int8) - 1).astype(np.float64)
+        return q64 @ pm.T
+    dot = (q64 @ np.asarray(x8).astype(np.float64).T).astype(np.float32).astype(np.float64)
+    nrm = int8_row_norms(x8)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        s = dot / nrm[None, :]
+    s[:, nrm == 0] = -np.inf
+    return s
+
+
+def exhaustive_topk(scores: np.ndarray, k: int):
+    """Top-k rows per query of an [nq, n] score matrix in the reference's order: Python's stable
+    ``sorted(..., reverse=True)`` over the rows in index order, i.e. (score desc, row asc)."""
+    n = scores.shape[1]
+    rows = np.arange(n)
+    out = []
+    for q in range(scores.shape[0]):
+        o = np.lexsort((rows, -scores[q]))[: min(k, n)]
+        out.append(o)
+    return np.array(out, dtype=np.int64)
+
+
 def int8_row_norms(x: np.ndarray) -> np.ndarray:
     """``np.linalg.norm(doc_int8)`` per row (float64), ``CohereEnhancedVectorDB.py:308``."""
     x = np.asarray(x)

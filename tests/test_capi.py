@@ -41,6 +41,13 @@ def test_workspace_sizes():
     assert ws == lib.vrq_hamming_topk_workspace_size(1_000_000, 128, 1024, 100)
     assert lib.vrq_search3_workspace_size(1000, 512, 1, 10) == 0      # dim unsupported
     assert lib.vrq_hamming_topk_workspace_size(10, 128, 1, 2000) == 0  # K > 1024
+    # exhaustive matrix-core scorer: pure function of the shape, 0 for unsupported shapes
+    g = lib.vrq_gemm_topk_workspace_size(3, 10_000_000, 1024, 1024, 10)
+    assert g > 1024 * 2048 and g == lib.vrq_gemm_topk_workspace_size(2, 10_000_000, 1024, 1024, 10)
+    assert lib.vrq_gemm_topk_workspace_size(3, 10_000_000, 1024, 1024, 10) < 4 << 30  # dense sample <= 2^21 cols
+    assert lib.vrq_gemm_topk_workspace_size(1, 1000, 1024, 1, 10) == 0
+    assert lib.vrq_gemm_topk_workspace_size(3, 1000, 1024, 1, 1025) == 0
+    assert lib.vrq_gemm_topk_workspace_size(3, 1 << 32, 1024, 1, 10) == 0
     n = 100_000_000
     per_q = lib.vrq_hamming_topk_workspace_size(n, 128, 1, 100) // (100 * 8)
     assert 1 <= per_q <= 4096
@@ -63,6 +70,18 @@ def test_workspace_sizes():
     (lambda L: L.vrq_merge_shards(0, 1, 1, None, None, None, None, None, 1, 1, None, None, None, None, None,
                                   None, None), N.VRQ_EINVAL),
     (lambda L: L.vrq_int8_row_norms(None, -1, 1024, None, None), N.VRQ_EINVAL),
+    (lambda L: L.vrq_gemm_topk(1, None, None, None, 10, 1024, 0, None, 1, 1, 0, None, None, None, None, 0, None),
+     N.VRQ_EINVAL),
+    (lambda L: L.vrq_gemm_topk(3, None, None, None, 10, 512, 0, None, 1, 1, 0, None, None, None, None, 0, None),
+     N.VRQ_EUNSUPPORTED),
+    (lambda L: L.vrq_gemm_topk(3, None, None, None, 10, 1024, 0, C.c_void_p(8), 1, 1, 0, C.c_void_p(8),
+                               C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), 0, None), N.VRQ_EINVAL),  # no x8
+    (lambda L: L.vrq_gemm_topk(2, C.c_void_p(8), None, None, 10, 1024, 0, C.c_void_p(8), 1, 2000, 0,
+                               C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), 1 << 30, None),
+     N.VRQ_EUNSUPPORTED),  # k > 1024
+    (lambda L: L.vrq_gemm_topk(2, C.c_void_p(8), None, None, 100_000, 1024, 0, C.c_void_p(8), 64, 10, 0,
+                               C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), 16, None),
+     N.VRQ_EWORKSPACE),
 ])
 def test_argument_validation(call, expect):
     assert call(N.load()) == expect

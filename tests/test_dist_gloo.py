@@ -137,3 +137,56 @@ def test_two_rank_gloo_sharded_search_equals_single_index():
         p.join(240)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+def _worker_c5(rank, world, port, result_q):
+    """Config 5 over 2 ranks: per-shard exact top-k (oracle stand-in for vrq_gemm_topk with the
+    shard's row_offset), ONE all-gather, merge_topk_shards == the single-corpus top-k."""
+    from vectorragquantization_amd.dist import gather_topk, merge_topk_shards
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    codes, x8, qf, _ = _corpus()
+    x8 = x8.copy()
+    x8[3000:3010] = 0                                   # zero-norm rows in shard 1
+    qf = qf.copy()
+    qf[0] = 0.0                                         # every score tied: row order decides
+    n, k = codes.shape[0], 10
+    r0, r1 = synth.shard_range(n, rank, world)
+    ok = True
+    for mode in ("binary", "int8_cosine"):
+        for kk in (k, 3000):                            # 3000 > shard rows: -1 / NaN padding
+            S = O.exhaustive_scores(mode, qf, codes=codes[r0:r1], x8=x8[r0:r1])
+            top = O.exhaustive_topk(S, kk)
+            rows = np.full((qf.shape[0], kk), -1, np.int64)
+            sc = np.full((qf.shape[0], kk), np.nan)
+            m = top.shape[1]
+            rows[:, :m] = top + r0
+            sc[:, :m] = np.take_along_axis(S, top, 1)
+            gr, gs = gather_topk(torch.from_numpy(rows), torch.from_numpy(sc))
+            cnt, mr, ms = (t.numpy() for t in merge_topk_shards(gr, gs, kk))
+            if rank == 0:
+                Sf = O.exhaustive_scores(mode, qf, codes=codes, x8=x8)
+                ref = O.exhaustive_topk(Sf, kk)
+                mm = ref.shape[1]
+                ok &= bool(np.all(cnt == mm))
+                ok &= np.array_equal(mr[:, :mm], ref)
+                ok &= np.array_equal(ms[:, :mm], np.take_along_axis(Sf, ref, 1))
+                ok &= bool(np.all(mr[:, mm:] == -1))
+    if rank == 0:
+        result_q.put(bool(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_config5_topk_merge_equals_single_corpus():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c5, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True

@@ -16,13 +16,14 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvrq.so")
 OBJDIR = os.path.join(PKG, "_obj")
-SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode.hip"]
+SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode.hip", "gemm_topk.hip"]
 ARCH = os.environ.get("VRQ_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 # per-source extras: the matrix-core scan keeps MFMA accumulators in VGPRs (the epilogue reads
 # them there; the AGPR form costs 16 v_accvgpr moves per accumulator use)
-EXTRA = {"hamming_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+EXTRA = {"hamming_mfma.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+         "gemm_topk.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _hipcc() -> str:

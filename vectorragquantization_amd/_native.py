@@ -26,6 +26,11 @@ VRQ_SCAN_STAGE_PREFIX = 16
 VRQ_SCAN_STAGE_MATRIX = 32
 VRQ_SCAN_STAGE_SUFFIX = 64
 VRQ_SCAN_STAGE_RECHECK = 128
+VRQ_GEMM_BINARY = 2
+VRQ_GEMM_INT8_COSINE = 3
+VRQ_GEMM_STAGE_SAMPLE = 16
+VRQ_GEMM_STAGE_MAIN = 32
+VRQ_GEMM_STAGE_FINISH = 64
 VRQ_SCAN_KIND_VALU = 0
 VRQ_SCAN_KIND_MFMA = 1
 
@@ -58,6 +63,9 @@ SIGNATURES = {
     "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),
     "vrq_encode": (C.c_int, [_I32, _P, _I64, _I32, _D, _P, _P, _P, _P]),
     "vrq_int8_row_norms": (C.c_int, [_P, _I64, _I32, _P, _P]),
+    "vrq_gemm_topk_workspace_size": (_SZ, [_I32, _I64, _I32, _I32, _I32]),
+    "vrq_gemm_topk": (C.c_int, [_I32, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,
+                                _P]),
 }
 
 

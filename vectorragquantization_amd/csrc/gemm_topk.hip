@@ -1,0 +1,774 @@
+// gemm_topk.hip -- K5 (BASELINE config 5): exhaustive Phase-II or Phase-III scoring of a batch of
+// queries against the WHOLE corpus on the matrix cores (v_mfma_i32_32x32x32_i8), with the top-k
+// fused in: the nq x n score matrix is never stored.
+//
+// Reference scores (exact_scores.h, bit-identical to the fused search's):
+//   VRQ_GEMM_BINARY       s = float(q . (2*unpackbits(code)-1)), float64   CohereEnhancedVectorDB.py:283-293
+//   VRQ_GEMM_INT8_COSINE  s = float32(q . int8) / ||int8||, -inf if 0      CohereEnhancedVectorDB.py:302-318
+// Result per query: the k rows with the largest s, ordered (s desc, row asc) -- the reference's
+// stable sorted(..., reverse=True) (:296, :321) over the rows taken in index order.
+//
+// Method (exact for every input):
+//  1. prep: q/S = a + b/256 + rho with S a power of two, a and b int8 "pieces" and rho the exact
+//     residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
+//     s' the reference score in the same units (Phase III: s/S; Phase II: (s + sum q)/(2S)):
+//       Phase III  Delta = ||rho||_2 (Cauchy-Schwarz; the score divides by ||x||_2) + f32 slack
+//       Phase II   Delta = ||rho||_1 (x in {0,1})                                  + f32 slack
+//  2. sample pass (dense): u for every (query, row) of an evenly spread row sample into dv, where
+//     u = fl(A_0 + A_1/256) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
+//     (x = the int8 row, or the code's bits expanded to 0/1 bytes).
+//  3. select: U = the k-th largest sample u of the query, thr = U - 2 Delta (rounded down).  k sample
+//     rows have s' >= U - Delta, so every row of the exact top-k -- ties with the k-th included --
+//     has u >= thr.
+//  4. main pass: every row with u >= thr is appended to a per-(query, chunk) candidate list.
+//  5. finish: exact reference scores of the candidates, sort by (s desc, row asc), first k.  A list
+//     overflow, more than FIN_CAP candidates, or fewer than min(k, n) of them (zero-norm rows,
+//     heavy ties) sends the query to the exact fallback: one workgroup scans every row.
+//
+// Work decomposition of the two matrix passes: one 256-thread workgroup per CU; each wave holds the
+// two int8 pieces of 32 queries for all of d = 1024 in the accumulator register file (256 AGPRs);
+// 32-row tiles stream HBM -> LDS by LDS-DMA (ring of 3, two tiles ahead) and every B fragment read
+// from LDS feeds both pieces' MFMAs.  Phase III reads the int8 rows as B directly (XOR-swizzled
+// image, conflict-free ds_read_b128); Phase II expands the packed bits into 0/1 bytes once per tile
+// (shared by the four waves) in a fixed k-permutation that the prep kernel applies to the query
+// pieces as well.  The threshold test of tile t-1 runs in tile t's MFMA shadow.
+#include <math.h>
+#include <stdlib.h>
+
+#include "exact_scores.h"
+#include "mfma_common.h"
+#include "vrq_internal.h"
+
+namespace vrq {
+namespace g5 {
+
+constexpr int GW = 4;                // waves per workgroup (one per SIMD)
+constexpr int GQW = 32;              // queries per wave (one 32-row M-block)
+constexpr int GQB = GW * GQW;        // queries per workgroup (128)
+constexpr int GRT = 32;              // corpus rows per tile (one 32-column N-block)
+constexpr int GKS = 32;              // k-steps of 32 dims (d = 1024)
+constexpr int NPK = 3;               // tile ring: DMA issued two tiles ahead
+constexpr int T3 = GRT * 1024;       // Phase-III tile: 32 int8 rows (32 KiB) ...
+constexpr int T3N = T3 + GRT * 8;    // ... + their 32 f64 norms
+constexpr int T2 = GRT * 128;        // Phase-II packed tile (4 KiB)
+constexpr int U2 = GKS * 1024;       // Phase-II unpacked tile [k-step][lane][16 B] (32 KiB)
+constexpr int FIN_CAP = 4096;        // candidates sorted in LDS per query by the finish kernel
+constexpr int FB_BATCH = 1024;       // rows per batch of the exact fallback
+constexpr int KMAX5 = 1024;          // k bound of the path
+constexpr int64_t kMinSample = 32768;
+constexpr int64_t kMaxSample = 1 << 21;
+constexpr int QA_BYTES = 2 * 1024;   // per query: piece 0 then piece 1, fragment order
+
+// Phase-II k-permutation inside a 32-dim k-step: fragment byte j = 4t + b of lane half h holds
+// bit 8b + t + 4h of the little-endian code dword (so a dword of the fragment is (w >> (t+4h)) &
+// 0x01010101, two VALU ops), i.e. packbits dim 8b + 7 - (t + 4h) of the step.
+__host__ __device__ constexpr int ph2_pos(int dim_in_step) {
+  const int b = dim_in_step >> 3, x = 7 - (dim_in_step & 7);  // byte, bit within the byte
+  const int h = x >> 2, t = x & 3;
+  return h * 16 + 4 * t + b;
+}
+
+__device__ __forceinline__ v16i mfma_i8(const v4i& a, const v4i& b, const v16i& c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void lds_read64(double& d, uint32_t a) {
+  asm volatile("ds_read_b64 %0, %1" : "=v"(d) : "v"(a) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void lds_read128_off(v4i& d, uint32_t a) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+
+// Monotone u32 image of a float for ASCENDING order; NaN -> 0 (below -inf).
+__device__ __forceinline__ uint32_t fkey(float u) {
+  const uint32_t b = __float_as_uint(u);
+  if ((b & 0x7fffffffu) > 0x7f800000u) return 0u;
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ double desc_key_inv(uint64_t key) {
+  const uint64_t a = ~key;
+  return __longlong_as_double((long long)((a & 0x8000000000000000ull) ? (a & 0x7fffffffffffffffull) : ~a));
+}
+
+// XCD-aware bijective block remap: consecutive logical blocks share one XCD's L2
+__device__ __forceinline__ int xcd_logical(int b, int nb) {
+  const int xcd = b & 7, slot = b >> 3, q8 = nb >> 3, r8 = nb & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+}
+
+// ---------------------------------------------------------------------------------------------
+// prep: one wave per (padded) query.  qa[q] = pieces a, b in fragment order (natural k order for
+// Phase III, ph2_pos for Phase II); delta[q] = Delta_q in u units.
+__global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* __restrict__ qf, int nq, int nq_pad,
+                                                        int8_t* __restrict__ qa, double* __restrict__ delta) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
+  if (q >= nq_pad) return;
+  int8_t* o = qa + (int64_t)q * QA_BYTES;
+  if (q >= nq) {  // padding queries: zero pieces (their thresholds never accept)
+    reinterpret_cast<int4*>(o)[l] = make_int4(0, 0, 0, 0);
+    reinterpret_cast<int4*>(o)[64 + l] = make_int4(0, 0, 0, 0);
+    if (l == 0) delta[q] = 0.0;
+    return;
+  }
+  float qv[DPL];
+  load_q(qv, qf + (int64_t)q * DIM);
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) mx = fmaxf(mx, fabsf(qv[i]));
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
+  // S = 2^e, the smallest power of two with max|q| / S <= 127 (exact scaling in f64)
+  int e = 0;
+  if (mx > 0.f) {
+    e = (int)ceil(log2((double)mx / 127.0));
+    while ((double)mx > 127.0 * ldexp(1.0, e)) ++e;
+    while ((double)mx <= 127.0 * ldexp(1.0, e - 1)) --e;
+  }
+  const double invS = ldexp(1.0, -e);
+  double r2 = 0.0, r1 = 0.0, q2 = 0.0, q1 = 0.0;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const double x = (double)qv[i] * invS;  // exact
+    const double a = rint(x);               // |a| <= 127
+    const double f = x - a;                 // exact, |f| <= 1/2
+    double b = rint(f * 256.0);
+    b = b > 127.0 ? 127.0 : (b < -127.0 ? -127.0 : b);
+    const double rho = f - b * (1.0 / 256.0);  // exact
+    r2 += rho * rho;
+    r1 += fabs(rho);
+    q2 += (double)qv[i] * (double)qv[i];
+    q1 += fabs((double)qv[i]);
+    const int dim = DPL * l + i, s = dim >> 5;
+    const int pos = s * 32 + (mode == VRQ_GEMM_BINARY ? ph2_pos(dim & 31) : (dim & 31));
+    o[pos] = (int8_t)a;
+    o[1024 + pos] = (int8_t)b;
+  }
+  r2 = wave_sum_f64(r2);
+  r1 = wave_sum_f64(r1);
+  q2 = wave_sum_f64(q2);
+  q1 = wave_sum_f64(q1);
+  constexpr double SLACK = 1.0 / (1 << 20);  // >= 16 f32 ulps of every rounding on the u path
+  if (l == 0) {
+    const double d = mode == VRQ_GEMM_BINARY ? r1 * (1.0 + SLACK) + SLACK * q1 * invS
+                                             : sqrt(r2) * (1.0 + SLACK) + SLACK * sqrt(q2) * invS;
+    delta[q] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The matrix pass.  PH = VRQ_GEMM_BINARY / VRQ_GEMM_INT8_COSINE; DENSE = the sample pass (u of
+// every (query, row) -> dv[q][chunk * chunk_rows + row]) else the thresholded pass (u >= thr[q] ->
+// candidate lists).  Chunk c covers rows [c * chunk_stride, + chunk_rows).
+template <int PH, bool DENSE>
+__global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
+    const uint8_t* __restrict__ src, const double* __restrict__ norms, int64_t n, const int8_t* __restrict__ qa,
+    int nq, const float* __restrict__ thr, uint32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
+    int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, float* __restrict__ dv, int64_t dv_stride) {
+  constexpr bool P3 = PH == VRQ_GEMM_INT8_COSINE;
+  constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
+  constexpr int SMEM = NPK * PKT + (P3 ? 0 : 2 * U2);
+  constexpr int PPW = P3 ? 9 : 1;                     // LDS-DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l = lane_id(), r = l & 31, h = l >> 5;
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int chunk = L / nqb, qb = L - chunk * nqb;
+  if (chunk >= nchunks) return;
+  const int64_t row0 = (int64_t)chunk * chunk_stride;
+  const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  if (row0 >= row1) return;
+  const int nrows = (int)(row1 - row0);
+  const int ntiles = (nrows + GRT - 1) / GRT;
+  const uint32_t sm0 = lds_addr(smem);
+
+  auto issue = [&](int t) {
+    uint8_t* buf = smem + (t % NPK) * PKT;
+    const int64_t tr0 = row0 + (int64_t)t * GRT;
+    if constexpr (P3) {
+      // row rr of the tile -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the row
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rr = w * 8 + i;
+        int64_t row = tr0 + rr;
+        row = row < row1 ? row : row1 - 1;
+        __builtin_amdgcn_global_load_lds(src + row * 1024 + ((l ^ (rr & 15)) << 4),
+                                         (__attribute__((address_space(3))) void*)(buf + rr * 1024), 16, 0, 0);
+      }
+      // the tile's 32 norms (every wave loads the same 256 B: equal DMA counts per wave)
+      int64_t nr = tr0 + (l >> 1);
+      nr = nr < row1 ? nr : row1 - 1;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1),
+                                       (__attribute__((address_space(3))) void*)(buf + T3), 4, 0, 0);
+    } else {
+      // rows 8w..8w+7: slot rr*8 + c' holds chunk c' ^ ((rr >> 1) & 7)
+      const int rr = 8 * w + (l >> 3), c = (l & 7) ^ ((rr >> 1) & 7);
+      int64_t row = tr0 + rr;
+      row = row < row1 ? row : row1 - 1;
+      __builtin_amdgcn_global_load_lds(src + row * 128 + c * 16,
+                                       (__attribute__((address_space(3))) void*)(buf + w * 1024), 16, 0, 0);
+    }
+  };
+
+  for (int t = 0; t < NPK - 1 && t < ntiles; ++t) issue(t);
+
+  // A fragments of this wave's 32 queries, both pieces, all 32 k-steps -> accumulator file
+  const int qbase = qb * GQB + w * GQW;
+  v4i A[2][GKS];
+  {
+    const int8_t* qp = qa + (int64_t)(qbase + r) * QA_BYTES + h * 16;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int s = 0; s < GKS; ++s) A[p][s] = *reinterpret_cast<const v4i*>(qp + p * 1024 + s * 32);
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int s = 0; s < GKS; ++s) asm volatile("" : "+a"(A[p][s]));
+  float th[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) th[g] = DENSE ? 0.f : thr[qbase + (g & 3) + 8 * (g >> 2) + 4 * h];
+
+  // Phase III: B fragment of k-step s for lane (r, h) = 16-B chunk 2s+h of tile row r, at slot
+  // r*64 + ((2s+h) ^ (r & 15)) = r*64 + 16*(s>>3) + off[s&7]
+  uint32_t boff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) boff[j] = (uint32_t)(((((2 * j) ^ (r & 14)) | (h ^ (r & 1))) << 4) + r * 1024);
+
+  v16i acc[2][2];        // [tile parity][piece]
+  float ures[16];        // u of the previous tile (flushed at the top of the next-but-one tile)
+  uint32_t hm = 0;       // hits of the previous tile: bit g = register g of this lane
+#pragma unroll
+  for (int g = 0; g < 16; ++g) ures[g] = 0.f;
+  float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk); Phase II 0 / NaN
+  const v16i zero = {};
+  const int64_t qstride = (int64_t)nchunks * capc;
+
+  // u of register g from the accumulators of one tile; NaN for rows without a score
+  auto uval = [&](const v16i& a0, const v16i& a1, int g, float inv) {
+    const float u = fmaf((float)a1[g], 1.0f / 256.0f, (float)a0[g]);
+    return P3 ? u * inv : u + inv;  // Phase II: inv is 0 (valid) or NaN
+  };
+  // results of tile tt (computed in the following tile's shadow) -> HBM
+  auto flush = [&](int tt) {
+    const int lr = tt * GRT + r;
+    if constexpr (DENSE) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int q = qbase + (g & 3) + 8 * (g >> 2) + 4 * h;
+        if (q < nq && lr < nrows) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[g];
+      }
+    } else {
+      if (__ballot(hm != 0)) {  // rare: ~k * n / sample rows per query over the corpus
+        uint32_t m = hm;
+        while (m) {
+          const int g = __builtin_ctz(m);
+          m &= m - 1;
+          const int q = qbase + (g & 3) + 8 * (g >> 2) + 4 * h;
+          const int pos = atomicAdd(ccnt + (int64_t)q * nchunks + chunk, 1);
+          if (pos < capc) cand[(int64_t)q * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + lr);
+        }
+        hm = 0;
+      }
+    }
+  };
+
+  auto tile = [&](auto PAR, int t) {
+    constexpr int p = decltype(PAR)::value;
+    // this wave's DMA of tile t landed (only tile t+1's may be outstanding; older stores too);
+    // after the barrier every wave's has, and every wave is done reading tile t-1's buffers
+    if (t + 1 < ntiles)
+      wait_vm<PPW>();
+    else
+      wait_vm<0>();
+    barrier_all();
+    if (t >= 2) flush(t - 2);
+    if (t + NPK - 1 < ntiles) issue(t + NPK - 1);  // into the slot of tile t-1
+    const uint32_t slot = sm0 + (uint32_t)((t % NPK) * PKT);
+    uint32_t bb;
+    if constexpr (P3) {
+      double nv;
+      lds_read64(nv, slot + T3 + (uint32_t)(r * 8));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nv)::"memory");
+      invc = (nv > 0.0 && t * GRT + r < nrows) ? (float)(1.0 / nv) : __builtin_nanf("");
+      bb = slot;
+    } else {
+      invc = (t * GRT + r < nrows) ? 0.f : __builtin_nanf("");
+      // expand the packed tile: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r,
+      // c = 2w + h (k-steps 4c..4c+3) and writes both lane halves' fragments of each
+      const int c = 2 * w + h;
+      v4i pv;
+      lds_read128(pv, slot + (uint32_t)((r * 8 + (c ^ ((r >> 1) & 7))) * 16));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv)::"memory");
+      const uint32_t ubw = sm0 + (uint32_t)(NPK * T2 + (t & 1) * U2);
+      const uint32_t wd[4] = {(uint32_t)pv.x, (uint32_t)pv.y, (uint32_t)pv.z, (uint32_t)pv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int s = 4 * c + i;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          v4i f;
+          f.x = (int)((wd[i] >> (4 * hh + 0)) & 0x01010101u);
+          f.y = (int)((wd[i] >> (4 * hh + 1)) & 0x01010101u);
+          f.z = (int)((wd[i] >> (4 * hh + 2)) & 0x01010101u);
+          f.w = (int)((wd[i] >> (4 * hh + 3)) & 0x01010101u);
+          lds_write128(ubw + (uint32_t)((s * 64 + hh * 32 + r) * 16), f);
+        }
+      }
+      wait_lgkm0();
+      barrier_all();
+      bb = ubw + (uint32_t)(l * 16);
+    }
+    v4i ring[4];
+    auto readB = [&](auto S) {
+      constexpr int s = decltype(S)::value;
+      if constexpr (P3)
+        lds_read128_off<(s >> 3) * 256>(ring[s & 3], bb + boff[s & 7]);
+      else
+        lds_read128_off<s * 1024>(ring[s & 3], bb);
+    };
+    readB(std::integral_constant<int, 0>{});
+    readB(std::integral_constant<int, 1>{});
+    VRQ_SCHED_FENCE();
+    static_for<0, GKS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      if constexpr (s + 2 < GKS) {
+        readB(std::integral_constant<int, s + 2>{});
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ring[s & 3])::"memory");
+      } else if constexpr (s + 1 < GKS) {
+        asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(ring[s & 3])::"memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ring[s & 3])::"memory");
+      }
+      acc[p][0] = mfma_i8(A[0][s], ring[s & 3], s == 0 ? zero : acc[p][0]);
+      acc[p][1] = mfma_i8(A[1][s], ring[s & 3], s == 0 ? zero : acc[p][1]);
+      asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
+      // threshold test / dense value of tile t-1, one register per k-step in 4..19
+      if constexpr (s >= 4 && s < 20) {
+        constexpr int g = s - 4;
+        if (t > 0) {
+          const float u = uval(acc[p ^ 1][0], acc[p ^ 1][1], g, invp);
+          if constexpr (DENSE)
+            ures[g] = u;
+          else
+            hm |= (u >= th[g] ? 1u : 0u) << g;
+        }
+      }
+      VRQ_SCHED_FENCE();
+    });
+    invp = invc;
+  };
+
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    tile(std::integral_constant<int, 1>{}, t + 1);
+  }
+  if (t < ntiles) tile(std::integral_constant<int, 0>{}, t);
+  wait_vm<0>();
+  // tile ntiles-2 (tested during the last tile), then the last tile itself
+  if (ntiles >= 2) flush(ntiles - 2);
+  const int pl = (ntiles - 1) & 1;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float u = pl ? uval(acc[1][0], acc[1][1], g, invp) : uval(acc[0][0], acc[0][1], g, invp);
+    if constexpr (DENSE)
+      ures[g] = u;
+    else
+      hm |= (u >= th[g] ? 1u : 0u) << g;
+  }
+  flush(ntiles - 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// select: per query, U = k-th largest valid sample u (3-pass radix select on the monotone key),
+// thr = U - 2 Delta rounded down (-inf when the sample holds fewer than k finite values); zeroes the
+// query's list lengths for the main pass.  Padding queries get thr = +inf.
+__global__ __launch_bounds__(256) void gemm_select_kernel(const float* __restrict__ dv, int64_t dv_stride,
+                                                          int64_t scr, int64_t sstride, int nsc, int64_t n, int k,
+                                                          const double* __restrict__ delta, float* __restrict__ thr,
+                                                          int32_t* __restrict__ ccnt, int nchunks, int nq) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t res[3];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  if (q >= nq) {
+    if (tid == 0) thr[q] = __builtin_inff();
+    return;
+  }
+  for (int i = tid; i < nchunks; i += 256) ccnt[(int64_t)q * nchunks + i] = 0;
+  const float* d = dv + (int64_t)q * dv_stride;
+  uint32_t prefix = 0, pmask = 0;
+  int kk = k;
+  bool ok = true;
+  constexpr int SH[3] = {21, 10, 0}, NBITS[3] = {11, 11, 10};
+  for (int pass = 0; pass < 3 && ok; ++pass) {
+    const int sh = SH[pass];
+    const uint32_t dm = (1u << NBITS[pass]) - 1;
+    for (int i = tid; i < 2048; i += 256) hist[i] = 0;
+    __syncthreads();
+    for (int c = 0; c < nsc; ++c) {
+      const int64_t rb = (int64_t)c * sstride;
+      const int64_t len = (rb + scr <= n) ? scr : (n > rb ? n - rb : 0);
+      const float* dc = d + (int64_t)c * scr;
+      for (int64_t i = tid; i < len; i += 256) {
+        const uint32_t key = fkey(dc[i]);
+        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> sh) & dm], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {  // top-down search: lane L owns bins [32L, 32L + 32)
+      uint32_t loc = 0;
+      for (int i = 0; i < 32; ++i) loc += hist[tid * 32 + i];
+      uint32_t suf = loc;  // inclusive suffix sum over lanes >= tid
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_down(suf, o, 64);
+        if (tid + o < 64) suf += y;
+      }
+      uint32_t above = suf - loc;
+      int found = -1;
+      uint32_t abv = 0;
+      for (int i = 31; i >= 0; --i) {
+        const uint32_t hc = hist[tid * 32 + i];
+        if (above < (uint32_t)kk && above + hc >= (uint32_t)kk) {
+          found = tid * 32 + i;
+          abv = above;
+        }
+        above += hc;
+      }
+      const uint64_t bal = __ballot(found >= 0);
+      if (tid == 0) res[0] = bal ? 1u : 0u;
+      if (found >= 0) {
+        res[1] = (uint32_t)found;
+        res[2] = abv;
+      }
+    }
+    __syncthreads();
+    if (!res[0]) {
+      ok = false;
+    } else {
+      const uint32_t b = res[1];
+      kk -= (int)res[2];
+      prefix |= b << sh;
+      pmask |= dm << sh;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    float t = -__builtin_inff();
+    if (ok && prefix != 0u) {
+      const double U = (double)fkey_inv(prefix);
+      t = __double2float_rd(U - 2.0 * delta[q]);
+    }
+    thr[q] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// exact (score desc, row asc) pair sort in LDS: ascending (key, row), key = desc_key_f64(score)
+__device__ inline void block_sort_pairs(uint64_t* key, uint32_t* row, int n_pow2) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < (n_pow2 >> 1); i += blockDim.x) {
+        const int lo = ((i / stride) * stride * 2) + (i % stride), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t ka = key[lo], kb = key[hi];
+        const uint32_t ra = row[lo], rb = row[hi];
+        const bool gt = ka > kb || (ka == kb && ra > rb);
+        if (gt == up) {
+          key[lo] = kb;
+          key[hi] = ka;
+          row[lo] = rb;
+          row[hi] = ra;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int PH>
+__device__ __forceinline__ double exact_score(const float (&qv)[DPL], const uint8_t* codes, const int8_t* x8,
+                                              const double* norms, int64_t row) {
+  if constexpr (PH == VRQ_GEMM_BINARY)
+    return phase2_dot(qv, codes + row * (DIM / 8));
+  else
+    return phase3_cos(qv, x8 + row * DIM, norms[row]);
+}
+
+struct FinShared {
+  uint64_t key[FIN_CAP];
+  uint32_t row[FIN_CAP];
+  int32_t misc[4];
+};
+
+// finish: candidates of the query -> exact scores -> sorted -> first min(k, n).  Flags the query for
+// the fallback instead when the candidates cannot be trusted to hold the top-k.
+template <int PH>
+__global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restrict__ codes,
+                                                          const int8_t* __restrict__ x8,
+                                                          const double* __restrict__ norms, int64_t n,
+                                                          int64_t row_offset, const float* __restrict__ qf, int k,
+                                                          const uint32_t* __restrict__ cand,
+                                                          const int32_t* __restrict__ ccnt, int nchunks, int capc,
+                                                          int32_t* __restrict__ out_count,
+                                                          int64_t* __restrict__ out_rows,
+                                                          double* __restrict__ out_scores,
+                                                          int32_t* __restrict__ fb_flag) {
+  __shared__ FinShared sh;
+  const int q = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  if (tid == 0) {
+    sh.misc[0] = 0;  // total
+    sh.misc[1] = 0;  // overflow
+    sh.misc[2] = 0;  // fill
+  }
+  __syncthreads();
+  const int32_t* cq = ccnt + (int64_t)q * nchunks;
+  for (int c = tid; c < nchunks; c += 256) {
+    const int v = cq[c];
+    atomicAdd(&sh.misc[0], v < capc ? v : capc);
+    if (v > capc) atomicOr(&sh.misc[1], 1);
+  }
+  __syncthreads();
+  const int total = sh.misc[0];
+  const int need = (int)((int64_t)k < n ? k : n);
+  if (sh.misc[1] || total > FIN_CAP || total < need) {
+    if (tid == 0) fb_flag[q] = 1;
+    return;
+  }
+  const uint32_t* Cq = cand + (int64_t)q * nchunks * capc;
+  for (int c = 0; c < nchunks; ++c) {
+    const int v = cq[c];
+    for (int i = tid; i < v; i += 256) sh.row[atomicAdd(&sh.misc[2], 1)] = Cq[(int64_t)c * capc + i];
+  }
+  __syncthreads();
+  float qv[DPL];
+  load_q(qv, qf + (int64_t)q * DIM);
+  for (int i = w; i < total; i += 4) {
+    const double s = exact_score<PH>(qv, codes, x8, norms, (int64_t)sh.row[i]);
+    if (l == 0) sh.key[i] = desc_key_f64(s);
+  }
+  const int np2 = next_pow2(total > 1 ? total : 1);
+  for (int i = total + tid; i < np2; i += 256) {
+    sh.key[i] = KEY_NONE;
+    sh.row[i] = 0xffffffffu;
+  }
+  __syncthreads();
+  block_sort_pairs(sh.key, sh.row, np2);
+  for (int i = tid; i < k; i += 256) {
+    const int64_t o = (int64_t)q * k + i;
+    out_rows[o] = i < need ? (int64_t)sh.row[i] + row_offset : -1;
+    out_scores[o] = i < need ? desc_key_inv(sh.key[i]) : __builtin_nan("");
+  }
+  if (tid == 0) {
+    out_count[q] = need;
+    fb_flag[q] = 0;
+  }
+}
+
+// fallback: exact running top-k over every row for the flagged queries (heavy ties, zero-norm rows,
+// list overflow).  One workgroup per query; rows enter the sort only when they beat the current k-th.
+template <int PH>
+__global__ __launch_bounds__(256) void gemm_fallback_kernel(const uint8_t* __restrict__ codes,
+                                                            const int8_t* __restrict__ x8,
+                                                            const double* __restrict__ norms, int64_t n,
+                                                            int64_t row_offset, const float* __restrict__ qf, int k,
+                                                            int32_t* __restrict__ out_count,
+                                                            int64_t* __restrict__ out_rows,
+                                                            double* __restrict__ out_scores,
+                                                            const int32_t* __restrict__ fb_flag) {
+  __shared__ uint64_t key[KMAX5 + FB_BATCH];
+  __shared__ uint32_t row[KMAX5 + FB_BATCH];
+  __shared__ int32_t fill;
+  const int q = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  if (!fb_flag[q]) return;
+  float qv[DPL];
+  load_q(qv, qf + (int64_t)q * DIM);
+  if (tid == 0) fill = 0;
+  int kc = 0;  // entries of the running top list key[0..kc)
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += FB_BATCH) {
+    const uint64_t kk = kc == k ? key[k - 1] : KEY_NONE;
+    const uint32_t kr = kc == k ? row[k - 1] : 0xffffffffu;
+    const int64_t end = base + FB_BATCH < n ? base + FB_BATCH : n;
+    for (int64_t rr = base + w; rr < end; rr += 4) {
+      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, codes, x8, norms, rr));
+      const bool take = kc < k || key_r < kk || (key_r == kk && (uint32_t)rr < kr);
+      if (take && l == 0) {
+        const int i = kc + atomicAdd(&fill, 1);
+        key[i] = key_r;
+        row[i] = (uint32_t)rr;
+      }
+    }
+    __syncthreads();
+    const int f = fill;
+    if (f > 0) {
+      const int tot = kc + f;
+      const int np2 = next_pow2(tot);
+      for (int i = tot + tid; i < np2; i += 256) {
+        key[i] = KEY_NONE;
+        row[i] = 0xffffffffu;
+      }
+      block_sort_pairs(key, row, np2);
+      kc = tot < k ? tot : k;
+    }
+    if (tid == 0) fill = 0;
+    __syncthreads();
+  }
+  for (int i = tid; i < k; i += 256) {
+    const int64_t o = (int64_t)q * k + i;
+    out_rows[o] = i < kc ? (int64_t)row[i] + row_offset : -1;
+    out_scores[o] = i < kc ? desc_key_inv(key[i]) : __builtin_nan("");
+  }
+  if (tid == 0) out_count[q] = kc;
+}
+
+// ---------------------------------------------------------------------------------------------
+struct GemmPlan {
+  int nqb, nq_pad;
+  int64_t scr, sstride, scols;  // sample: nsc chunks of scr rows, chunk c at row c * sstride
+  int nsc;
+  int64_t chunk_rows;
+  int nchunks, capc;
+  size_t off_delta, off_thr, off_flag, off_cnt, off_cand, off_dv, bytes;
+};
+
+static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
+  if (n < 1 || n >= (int64_t(1) << 32) || nq < 1 || k < 1 || k > KMAX5) return VRQ_EUNSUPPORTED;
+  p->nqb = (nq + GQB - 1) / GQB;
+  p->nq_pad = p->nqb * GQB;
+  const int want = 256 / p->nqb > 0 ? 256 / p->nqb : 1;  // chunks per query block: one WG per CU
+  // sample rows: expected candidates k * n / S ~ FIN_CAP / 4 (VRQ_GEMM_SAMPLE_DIV overrides n / S)
+  int64_t S = (int64_t)(4.0 * (double)k * (double)n / (double)FIN_CAP);
+  const char* ev = getenv("VRQ_GEMM_SAMPLE_DIV");
+  if (ev && atoi(ev) >= 1) S = n / atoi(ev);
+  if (S < kMinSample) S = kMinSample;
+  if (S > kMaxSample) S = kMaxSample;
+  if (S > n) S = n;
+  int64_t nsc = want;
+  int64_t scr = ((S + nsc - 1) / nsc + GRT - 1) / GRT * GRT;
+  nsc = (S + scr - 1) / scr;
+  p->scr = scr;
+  p->nsc = (int)nsc;
+  p->sstride = n / nsc >= scr ? n / nsc : scr;  // chunks never overlap; the last may be cut at n
+  p->scols = nsc * scr;
+  int64_t cr = (n + want - 1) / want;
+  cr = (cr + GRT - 1) / GRT * GRT;
+  p->chunk_rows = cr;
+  p->nchunks = (int)((n + cr - 1) / cr);
+  const int64_t Sv = S < n ? S : n;
+  const int64_t expect = ((int64_t)k * cr + Sv - 1) / Sv;
+  int capc = 64;
+  while (capc < 4 * expect && capc < 4096) capc <<= 1;
+  p->capc = capc;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t qa = al((size_t)p->nq_pad * QA_BYTES);
+  p->off_delta = qa;
+  p->off_thr = p->off_delta + al((size_t)p->nq_pad * sizeof(double));
+  p->off_flag = p->off_thr + al((size_t)p->nq_pad * sizeof(float));
+  p->off_cnt = p->off_flag + al((size_t)nq * sizeof(int32_t));
+  p->off_cand = p->off_cnt + al((size_t)nq * p->nchunks * sizeof(int32_t));
+  p->off_dv = p->off_cand + al((size_t)nq * p->nchunks * p->capc * sizeof(uint32_t));
+  p->bytes = p->off_dv + al((size_t)nq * p->scols * sizeof(float));
+  return VRQ_OK;
+}
+
+}  // namespace g5
+}  // namespace vrq
+
+using namespace vrq;
+using namespace vrq::g5;
+
+extern "C" size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k) {
+  GemmPlan p;
+  if ((mode != VRQ_GEMM_BINARY && mode != VRQ_GEMM_INT8_COSINE) || dim != DIM || gemm_plan(n, nq, k, &p) != VRQ_OK)
+    return 0;
+  return p.bytes;
+}
+
+extern "C" int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
+                             int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
+                             int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  if (mode != VRQ_GEMM_BINARY && mode != VRQ_GEMM_INT8_COSINE) return VRQ_EINVAL;
+  if (dim != DIM) return VRQ_EUNSUPPORTED;
+  VRQ_CHECK_ARG(qf && out_count && out_rows && out_scores && workspace && n > 0 && nq > 0 && k > 0);
+  if (mode == VRQ_GEMM_BINARY) VRQ_CHECK_ARG(codes);
+  if (mode == VRQ_GEMM_INT8_COSINE) VRQ_CHECK_ARG(x8 && norms);
+  GemmPlan p;
+  const int rc = gemm_plan(n, nq, k, &p);
+  if (rc != VRQ_OK) return rc;
+  if (workspace_bytes < p.bytes) return VRQ_EWORKSPACE;
+  constexpr int ALL = VRQ_GEMM_STAGE_SAMPLE | VRQ_GEMM_STAGE_MAIN | VRQ_GEMM_STAGE_FINISH;
+  const int st = (flags & ALL) ? (flags & ALL) : ALL;
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)workspace;
+  int8_t* qa = (int8_t*)ws;
+  double* delta = (double*)(ws + p.off_delta);
+  float* thr = (float*)(ws + p.off_thr);
+  int32_t* flag = (int32_t*)(ws + p.off_flag);
+  int32_t* cnt = (int32_t*)(ws + p.off_cnt);
+  uint32_t* cand = (uint32_t*)(ws + p.off_cand);
+  float* dv = (float*)(ws + p.off_dv);
+  const bool P3 = mode == VRQ_GEMM_INT8_COSINE;
+  const uint8_t* src = P3 ? (const uint8_t*)x8 : codes;
+  const dim3 blk(GW * 64);
+  if (st & VRQ_GEMM_STAGE_SAMPLE) {
+    hipLaunchKernelGGL(gemm_prep_kernel, dim3((p.nq_pad + 3) / 4), dim3(256), 0, s, mode, qf, nq, p.nq_pad, qa,
+                       delta);
+    VRQ_LAUNCH_CHECK();
+    const dim3 grid(p.nsc * p.nqb);
+    if (P3)
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, true>), grid, blk, 0, s, src, norms, n, qa, nq,
+                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
+                         p.nqb, dv, p.scols);
+    else
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, true>), grid, blk, 0, s, src, norms, n, qa, nq,
+                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
+                         p.nqb, dv, p.scols);
+    VRQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, p.scr,
+                       p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq);
+    VRQ_LAUNCH_CHECK();
+  }
+  if (st & VRQ_GEMM_STAGE_MAIN) {
+    const dim3 grid(p.nchunks * p.nqb);
+    if (P3)
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, false>), grid, blk, 0, s, src, norms, n, qa, nq,
+                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                         (float*)nullptr, (int64_t)0);
+    else
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, false>), grid, blk, 0, s, src, norms, n, qa, nq,
+                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                         (float*)nullptr, (int64_t)0);
+    VRQ_LAUNCH_CHECK();
+  }
+  if (st & VRQ_GEMM_STAGE_FINISH) {
+    // VRQ_GEMM_FALLBACK=0 (tests only, read per call): skip the exact fallback, leaving flagged
+    // queries' outputs unwritten, to prove the matrix-core path alone served a batch
+    const char* fe = getenv("VRQ_GEMM_FALLBACK");
+    const bool fb = !(fe && fe[0] == '0');
+    if (P3) {
+      hipLaunchKernelGGL(gemm_finish_kernel<VRQ_GEMM_INT8_COSINE>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
+                         row_offset, qf, k, (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count,
+                         out_rows, out_scores, flag);
+      VRQ_LAUNCH_CHECK();
+      if (fb)
+        hipLaunchKernelGGL(gemm_fallback_kernel<VRQ_GEMM_INT8_COSINE>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
+                         row_offset, qf, k, out_count, out_rows, out_scores, (const int32_t*)flag);
+    } else {
+      hipLaunchKernelGGL(gemm_finish_kernel<VRQ_GEMM_BINARY>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
+                         row_offset, qf, k, (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count,
+                         out_rows, out_scores, flag);
+      VRQ_LAUNCH_CHECK();
+      if (fb)
+        hipLaunchKernelGGL(gemm_fallback_kernel<VRQ_GEMM_BINARY>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
+                         row_offset, qf, k, out_count, out_rows, out_scores, (const int32_t*)flag);
+    }
+    VRQ_LAUNCH_CHECK();
+  }
+  return VRQ_OK;
+}

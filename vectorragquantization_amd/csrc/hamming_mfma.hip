@@ -30,8 +30,7 @@
 //    K-list per query, exactly in every case (overflow -> exact rescan).
 #include <stdlib.h>
 
-#include <type_traits>
-
+#include "mfma_common.h"
 #include "vrq_internal.h"
 #include "vrq_scan.h"
 
@@ -44,9 +43,6 @@
 
 namespace vrq {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v8i __attribute__((ext_vector_type(8)));
-typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int MWAVES = 4;                   // waves per workgroup (one per SIMD)
 constexpr int QPW = 64;                     // queries per wave (2 M-blocks of 32)
@@ -75,23 +71,6 @@ constexpr int E8M0_TWO = 128;               // MX block scale 2^1
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
 
-// compile-time loop: f(integral_constant<int, I>) for I in [I0, N) -- every index a constant,
-// so register arrays indexed by it stay in registers (a #pragma unroll may give up)
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-__device__ __forceinline__ void barrier_all() { asm volatile("s_barrier" ::: "memory"); }
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 // 32 code bits -> one FP4 MFMA fragment lane: 32 e2m1 values, code 0x1 (0.5) per set bit.
 // Dword j, nibble i holds bit 4i + j: a fixed permutation of k applied identically to queries
 // (A) and rows (B), so every dot product is unchanged.
@@ -112,32 +91,6 @@ __device__ __forceinline__ v16f mfma_fp4(const v4i& a, const v4i& b, const v16f&
   return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, FMT_FP4, FMT_FP4, 0, E8M0_TWO, 0, E8M0_TWO);
 }
 
-// LDS accesses inside the tile loop are inline asm: after a global_load_lds the compiler
-// would otherwise put s_waitcnt vmcnt(0) before the next LDS access (it cannot tell the
-// DMA's target apart), stalling every tile on the DMA just issued.  Loaded registers become
-// valid at the matching wait, which takes them as "+v" operands so no use is hoisted above it.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
-}
-__device__ __forceinline__ void lds_read128(v4i& d, uint32_t a) {
-  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(a) : "memory");
-}
-__device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
-  asm volatile("ds_read_b32 %0, %1" : "=v"(d) : "v"(a) : "memory");
-}
-__device__ __forceinline__ void lds_write128(uint32_t a, const v4i& v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_write32(uint32_t a, int v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_add32(uint32_t a, int v) {
-  asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_add_rtn32(int& d, uint32_t a, int v) {
-  asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(v) : "memory");
-}
-#define VRQ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // Packed tile image: 16-byte piece c of tile row r lives at slot r*8 + (c ^ ((r>>1)&7)).
 __device__ __forceinline__ int pk_slot(int r, int c) { return r * 8 + (c ^ ((r >> 1) & 7)); }

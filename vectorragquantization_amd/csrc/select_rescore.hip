@@ -17,6 +17,7 @@
 // BLAS summation order, <= a few ulp away: the 1e-5 tolerance of the north
 // star).  The norm is sqrt of an exact integer sum (correctly rounded, equal
 // to np.linalg.norm) and the division is IEEE double, as in the reference.
+#include "exact_scores.h"
 #include "vrq_internal.h"
 #include "vrq_scan.h"
 
@@ -27,8 +28,6 @@ constexpr int KMAX = 1024;          // max K (binary_k) handled per query
 constexpr int MAX_LISTS = 4096;     // max chunk lists merged per query
 constexpr int NBINS = 1025 + 3;     // dist in [0, 1024] for 1024-bit codes
 constexpr uint64_t ROW_MASK = (1ull << KEY_ROW_BITS) - 1;
-constexpr int DIM = 1024;           // embedding dim of the fused kernels
-constexpr int DPL = DIM / WAVE;     // dims per lane (16)
 
 // Per-query LDS state, sized for at most KM candidates (binary_k) and ML lists.  The general
 // instance (KMAX, MAX_LISTS) takes ~89 KiB, one workgroup per CU; the common shape (K <= 128,
@@ -235,49 +234,6 @@ __device__ void stable_desc_order(const double* sc, int m, SH& sh) {
     }
   }
   __syncthreads();
-}
-
-// Phase II score of one code row for the lane-resident query slice (dims 16l..16l+15).
-__device__ __forceinline__ double phase2_dot(const float (&qv)[DPL], const uint8_t* __restrict__ code_row) {
-  const int l = lane_id();
-  const uint16_t b = *reinterpret_cast<const uint16_t*>(code_row + 2 * l);  // bytes 2l, 2l+1
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) {
-    // packbits is MSB-first: dim 16l+i lives in byte 2l + i/8 at bit 7 - i%8
-    const int bit = (i < 8) ? ((b >> (7 - i)) & 1) : ((b >> (8 + 15 - i)) & 1);
-    s += bit ? (double)qv[i] : -(double)qv[i];
-  }
-  return wave_sum_f64(s);
-}
-
-// Phase III: float32(q . int8 row) / norm, -inf if norm == 0.
-__device__ __forceinline__ double phase3_cos(const float (&qv)[DPL], const int8_t* __restrict__ xrow, double nrm) {
-  const int l = lane_id();
-  const int4 raw = *reinterpret_cast<const int4*>(xrow + DPL * l);
-  const int32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) {
-    const int8_t x = (int8_t)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
-    s += (double)qv[i] * (double)x;  // exact product
-  }
-  s = wave_sum_f64(s);                // exact sum
-  const float f = (float)s;           // one rounding: correctly rounded float32 dot
-  return nrm == 0.0 ? -__builtin_inf() : (double)f / nrm;
-}
-
-__device__ __forceinline__ void load_q(float (&qv)[DPL], const float* __restrict__ q) {
-  const int l = lane_id();
-  const float4* p = reinterpret_cast<const float4*>(q + DPL * l);
-#pragma unroll
-  for (int i = 0; i < DPL / 4; ++i) {
-    const float4 v = p[i];
-    qv[4 * i + 0] = v.x;
-    qv[4 * i + 1] = v.y;
-    qv[4 * i + 2] = v.z;
-    qv[4 * i + 3] = v.w;
-  }
 }
 
 // Finish one query from Phase-I candidates sh.sel[0..Kp) with s2 (and s3 where needed)

@@ -53,7 +53,9 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 }
 
 // Sortable 64-bit image of a double for DESCENDING order: larger double -> smaller key.
+// -0.0 maps to the key of +0.0: Python's sort (the reference) treats them as equal.
 __device__ __forceinline__ uint64_t desc_key_f64(double x) {
+  if (x == 0.0) x = 0.0;
   uint64_t u = (uint64_t)__double_as_longlong(x);
   u = (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);  // ascending image
   return ~u;                                                            // descending

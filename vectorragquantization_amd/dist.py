@@ -89,6 +89,36 @@ def merge_shards(cnt, rows, d, s2, s3, k: int, K3: int):
     return oc, orow, od, o2, o3, src
 
 
+def merge_topk_shards(rows: torch.Tensor, scores: torch.Tensor, k: int):
+    """Merge of row-sharded ``vrq_gemm_topk`` outputs (config 5) after the all-gather.
+
+    ``rows``/``scores`` are [S, nq, k] (global rows; -1 / NaN padding).  Result: (count, rows,
+    scores) of the global top-k in the reference's (score desc, row asc) order, identical to one
+    call over the whole corpus.  Two stable sorts: by row (padding last), then by score descending
+    (-0.0 equal to +0.0 and padding equal to -inf, both as in Python's sort; padding stays behind
+    real -inf rows because it is last in row order)."""
+    S, nq, kk = rows.shape
+    r = rows.permute(1, 0, 2).reshape(nq, S * kk)
+    sc = scores.permute(1, 0, 2).reshape(nq, S * kk)
+    o = torch.sort(torch.where(r >= 0, r, torch.full_like(r, torch.iinfo(torch.int64).max)), dim=1,
+                   stable=True).indices
+    r, sc = torch.gather(r, 1, o), torch.gather(sc, 1, o)
+    key = torch.where(r >= 0, sc, torch.full_like(sc, float("-inf"))) + 0.0  # + 0.0 maps -0.0 to +0.0
+    o = torch.sort(-key, dim=1, stable=True).indices[:, :k]
+    r, sc = torch.gather(r, 1, o), torch.gather(sc, 1, o)
+    return (r >= 0).sum(1).to(torch.int32), r, sc
+
+
+def gather_topk(rows: torch.Tensor, scores: torch.Tensor, group=None):
+    """One all-gather of a rank's [nq, k] (rows i64, scores f64) -> stacked [S, nq, k] each."""
+    S = dist.get_world_size(group)
+    buf = torch.cat([rows.contiguous().view(torch.uint8).reshape(-1), scores.contiguous().view(torch.uint8).reshape(-1)])
+    out = gather_candidates(buf, group).reshape(S, -1)
+    h = rows.numel() * 8
+    return (out[:, :h].contiguous().view(torch.int64).reshape(S, *rows.shape),
+            out[:, h:].contiguous().view(torch.float64).reshape(S, *scores.shape))
+
+
 class ShardedSearch:
     """One rank's shard of a row-sharded corpus + the collective search."""
 

@@ -59,6 +59,33 @@ class SearchBatch:
         return out
 
 
+def gemm_topk(mode: str, qf: torch.Tensor, k: int, codes: torch.Tensor | None = None,
+              x8: torch.Tensor | None = None, norms: torch.Tensor | None = None, row_offset: int = 0,
+              flags: int = 0, workspace: torch.Tensor | None = None):
+    """Exhaustive Phase-II (``mode="binary"``) or Phase-III (``mode="int8_cosine"``) top-k of a query
+    batch over EVERY row on the matrix cores (``vrq_gemm_topk``, BASELINE config 5): the scores of
+    ``CohereEnhancedVectorDB.py:283-293`` / ``:302-318`` ordered like the reference's stable
+    ``sorted(..., reverse=True)`` over rows in index order.  Returns (count i32[nq], rows i64[nq, k],
+    scores f64[nq, k]) device tensors."""
+    m = {"binary": N.VRQ_GEMM_BINARY, "int8_cosine": N.VRQ_GEMM_INT8_COSINE}[mode]
+    src = codes if m == N.VRQ_GEMM_BINARY else x8
+    dev = qf.device
+    nq, n = qf.shape[0], src.shape[0]
+    cnt = torch.full((nq,), -2, dtype=torch.int32, device=dev)  # -2: never written
+    rows = torch.full((nq, k), -2, dtype=torch.int64, device=dev)
+    scores = torch.empty((nq, k), dtype=torch.float64, device=dev)
+    lib = N.load()
+    need = lib.vrq_gemm_topk_workspace_size(m, n, qf.shape[1], nq, k)
+    if need == 0:
+        raise N.VrqNativeError(f"vrq_gemm_topk: unsupported shape n={n} dim={qf.shape[1]} nq={nq} k={k}")
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty((need,), dtype=torch.uint8, device=dev)
+    N.check(lib.vrq_gemm_topk(m, N.ptr(codes), N.ptr(x8), N.ptr(norms), n, qf.shape[1], row_offset, N.ptr(qf), nq,
+                              k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores), N.ptr(workspace),
+                              workspace.numel(), N.stream_handle(dev)), "vrq_gemm_topk")
+    return cnt, rows, scores
+
+
 def search3(codes: torch.Tensor, x8: torch.Tensor, norms: torch.Tensor, qf: torch.Tensor, qb: torch.Tensor,
             k: int, K: int, K3: int, flags: int = 0, row_offset: int = 0, rescore_row: torch.Tensor | None = None,
             workspace: torch.Tensor | None = None):
