@@ -191,7 +191,7 @@ int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, vo
  * row asc) -- the reference's stable sorted(..., reverse=True) (:296, :321) over rows in index
  * order -- as row_offset + row, with their exact scores (bit-identical to vrq_search3's);
  * out_count i32[nq] = min(k, n); unused slots -1 / NaN.  Queries must be finite.
- * Exact for every input: int8-split queries on v_mfma_i32_32x32x32_i8 give scores within a
+ * Exact for every input: int8-quantised queries on v_mfma_i32_32x32x32_i8 give scores within a
  * proven per-query bound, a sampled threshold keeps every row that can reach the top-k, and the
  * survivors are rescored exactly (heavy-tie inputs fall back to an exact scan of every row).
  * flags: 0, or a subset of the VRQ_GEMM_STAGE_* (issued in order = the full call).
@@ -203,6 +203,9 @@ int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, vo
 #define VRQ_GEMM_STAGE_MAIN 32   /* thresholded pass over every row -> candidate lists */
 #define VRQ_GEMM_STAGE_FINISH 64 /* exact rescoring + sort of the candidates (+ exact fallback) */
 size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k);
+/* int8 pieces per query of this build's matrix pass (1: q ~ S*a, 2: q ~ S*(a + b/256)); the
+ * algorithmic ops of a pass are 2*nq*n*dim either way (for roofline reporting) */
+int vrq_gemm_topk_pieces(void);
 int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
                   int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
                   int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,

@@ -9,13 +9,13 @@
 // stable sorted(..., reverse=True) (:296, :321) over the rows taken in index order.
 //
 // Method (exact for every input):
-//  1. prep: q/S = a + b/256 + rho with S a power of two, a and b int8 "pieces" and rho the exact
-//     residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
+//  1. prep: q/S = a + rho (one int8 "piece", S = max|q|/127; the two-piece build adds b/256 with S
+//     a power of two) and rho the exact residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
 //     s' the reference score in the same units (Phase III: s/S; Phase II: (s + sum q)/(2S)):
 //       Phase III  Delta = ||rho||_2 (Cauchy-Schwarz; the score divides by ||x||_2) + f32 slack
 //       Phase II   Delta = ||rho||_1 (x in {0,1})                                  + f32 slack
 //  2. sample pass (dense): u for every (query, row) of an evenly spread row sample into dv, where
-//     u = fl(A_0 + A_1/256) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
+//     u = fl(A_0 [+ A_1/256]) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
 //     (x = the int8 row, or the code's bits expanded to 0/1 bytes).
 //  3. select: U = the k-th largest sample u of the query, thr = U - 2 Delta (rounded down).  k sample
 //     rows have s' >= U - Delta, so every row of the exact top-k -- ties with the k-th included --
@@ -26,9 +26,9 @@
 //     heavy ties) sends the query to the exact fallback: one workgroup scans every row.
 //
 // Work decomposition of the two matrix passes: one 256-thread workgroup per CU; each wave holds the
-// two int8 pieces of 32 queries for all of d = 1024 in the accumulator register file (256 AGPRs);
-// 32-row tiles stream HBM -> LDS by LDS-DMA (ring of 3, two tiles ahead) and every B fragment read
-// from LDS feeds both pieces' MFMAs.  Phase III reads the int8 rows as B directly (XOR-swizzled
+// int8 piece of 64 queries (two pieces of 32) for all of d = 1024 in the accumulator file (256 AGPRs);
+// 32-row tiles stream HBM -> LDS by LDS-DMA (2-3 tiles ahead, pieces spread over the MFMA shadow) and every B fragment read
+// from LDS feeds two MFMAs (both M-blocks, or both pieces).  Phase III reads the int8 rows as B directly (XOR-swizzled
 // image, conflict-free ds_read_b128); Phase II expands the packed bits into 0/1 bytes once per tile
 // (shared by the four waves) in a fixed k-permutation that the prep kernel applies to the query
 // pieces as well.  The threshold test of tile t-1 runs in tile t's MFMA shadow.
@@ -39,25 +39,50 @@
 #include "mfma_common.h"
 #include "vrq_internal.h"
 
+// tools/build_g5_variants.sh compiles this file with VRQ_G5_BISECT bits set to time the matrix pass
+// with parts removed (1: threshold test, 2: LDS-DMA, 4: tile barrier, 8: MFMA; 2/4/8 give wrong
+// results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
+// the library build.
+#ifndef VRQ_G5_BISECT
+#define VRQ_G5_BISECT 0
+#endif
+#ifndef VRQ_G5_BAHEAD
+#define VRQ_G5_BAHEAD 2
+#endif
+#ifndef VRQ_G5_PIECES
+#define VRQ_G5_PIECES 1
+#endif
+
 namespace vrq {
 namespace g5 {
 
 constexpr int GW = 4;                // waves per workgroup (one per SIMD)
-constexpr int GQW = 32;              // queries per wave (one 32-row M-block)
-constexpr int GQB = GW * GQW;        // queries per workgroup (128)
+// int8 pieces per query: 2 (q/S = a + b/256 + rho, 16-bit split, 32 queries per wave) or 1 (q/S =
+// a + rho, 64 queries per wave: half the MFMA work and twice the corpus-byte reuse per query, a
+// ~4x wider threshold margin -> ~2K exact rescorings per query at 10M rows).  Either way the A
+// fragments fill the 256 accumulator registers.  Measured at 10M x 1024, nq = 1024 (both phases):
+// one piece 29.3 ms, two pieces 40.6 ms per batch -> one piece is the library build.
+constexpr int NPC = VRQ_G5_PIECES;
+constexpr int NMB = 3 - NPC;         // 32-query M-blocks per wave
+constexpr int GQW = 32 * NMB;        // queries per wave
+constexpr int GQB = GW * GQW;        // queries per workgroup
+constexpr int NE = 16 * NMB;         // threshold tests per lane per tile
+// candidates sorted in LDS per query by the finish kernel, and the per-(query, chunk) list capacity
+// as a multiple of the hits the sample predicts (one piece: ~4x wider margin)
+constexpr int FIN_CAP = NPC == 2 ? 4096 : 8192;
+constexpr int CAP_MULT = NPC == 2 ? 4 : 16;
 constexpr int GRT = 32;              // corpus rows per tile (one 32-column N-block)
 constexpr int GKS = 32;              // k-steps of 32 dims (d = 1024)
-constexpr int NPK = 3;               // tile ring: DMA issued two tiles ahead
 constexpr int T3 = GRT * 1024;       // Phase-III tile: 32 int8 rows (32 KiB) ...
 constexpr int T3N = T3 + GRT * 8;    // ... + their 32 f64 norms
 constexpr int T2 = GRT * 128;        // Phase-II packed tile (4 KiB)
 constexpr int U2 = GKS * 1024;       // Phase-II unpacked tile [k-step][lane][16 B] (32 KiB)
-constexpr int FIN_CAP = 4096;        // candidates sorted in LDS per query by the finish kernel
+
 constexpr int FB_BATCH = 1024;       // rows per batch of the exact fallback
 constexpr int KMAX5 = 1024;          // k bound of the path
 constexpr int64_t kMinSample = 32768;
 constexpr int64_t kMaxSample = 1 << 21;
-constexpr int QA_BYTES = 2 * 1024;   // per query: piece 0 then piece 1, fragment order
+constexpr int QA_BYTES = NPC * 1024; // per query: piece 0 (then piece 1), fragment order
 
 // Phase-II k-permutation inside a 32-dim k-step: fragment byte j = 4t + b of lane half h holds
 // bit 8b + t + 4h of the little-endian code dword (so a dword of the fragment is (w >> (t+4h)) &
@@ -109,7 +134,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   int8_t* o = qa + (int64_t)q * QA_BYTES;
   if (q >= nq) {  // padding queries: zero pieces (their thresholds never accept)
     reinterpret_cast<int4*>(o)[l] = make_int4(0, 0, 0, 0);
-    reinterpret_cast<int4*>(o)[64 + l] = make_int4(0, 0, 0, 0);
+    if (NPC == 2) reinterpret_cast<int4*>(o)[64 + l] = make_int4(0, 0, 0, 0);
     if (l == 0) delta[q] = 0.0;
     return;
   }
@@ -120,21 +145,23 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   for (int i = 0; i < DPL; ++i) mx = fmaxf(mx, fabsf(qv[i]));
 #pragma unroll
   for (int m = 1; m < WAVE; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
-  // S = 2^e, the smallest power of two with max|q| / S <= 127 (exact scaling in f64)
+  // two pieces: S = 2^e, the smallest power of two with max|q| / S <= 127 (exact scaling in f64);
+  // one piece: S = max|q| / 127 (the rounding of q/S in f64 is far inside the slack below)
   int e = 0;
   if (mx > 0.f) {
     e = (int)ceil(log2((double)mx / 127.0));
     while ((double)mx > 127.0 * ldexp(1.0, e)) ++e;
     while ((double)mx <= 127.0 * ldexp(1.0, e - 1)) --e;
   }
-  const double invS = ldexp(1.0, -e);
+  const double invS = NPC == 2 ? ldexp(1.0, -e) : (mx > 0.f ? 127.0 / (double)mx : 1.0);
   double r2 = 0.0, r1 = 0.0, q2 = 0.0, q1 = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    const double x = (double)qv[i] * invS;  // exact
-    const double a = rint(x);               // |a| <= 127
+    const double x = (double)qv[i] * invS;  // exact for two pieces
+    double a = rint(x);                     // |a| <= 127
+    a = a > 127.0 ? 127.0 : (a < -127.0 ? -127.0 : a);
     const double f = x - a;                 // exact, |f| <= 1/2
-    double b = rint(f * 256.0);
+    double b = NPC == 2 ? rint(f * 256.0) : 0.0;
     b = b > 127.0 ? 127.0 : (b < -127.0 ? -127.0 : b);
     const double rho = f - b * (1.0 / 256.0);  // exact
     r2 += rho * rho;
@@ -144,7 +171,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     const int dim = DPL * l + i, s = dim >> 5;
     const int pos = s * 32 + (mode == VRQ_GEMM_BINARY ? ph2_pos(dim & 31) : (dim & 31));
     o[pos] = (int8_t)a;
-    o[1024 + pos] = (int8_t)b;
+    if (NPC == 2) o[1024 + pos] = (int8_t)b;
   }
   r2 = wave_sum_f64(r2);
   r1 = wave_sum_f64(r1);
@@ -168,10 +195,16 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     int nq, const float* __restrict__ thr, uint32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, float* __restrict__ dv, int64_t dv_stride) {
   constexpr bool P3 = PH == VRQ_GEMM_INT8_COSINE;
+  // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
+  // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
+  // packed tile t+1 expanded into the unpacked ring (2 tiles) during tile t.
+  constexpr int NP = P3 ? 3 : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
-  constexpr int SMEM = NPK * PKT + (P3 ? 0 : 2 * U2);
+  constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
   constexpr int PPW = P3 ? 9 : 1;                     // LDS-DMA instructions per wave per tile
+  constexpr int AHEAD = NP - 1;                       // tiles the DMA runs ahead
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+  __shared__ int32_t lcnt[GW * GQW];  // per-(query, this chunk) list lengths, one row of 32 per wave
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l = lane_id(), r = l & 31, h = l >> 5;
   const int L = xcd_logical(blockIdx.x, gridDim.x);
@@ -184,53 +217,85 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   const int ntiles = (nrows + GRT - 1) / GRT;
   const uint32_t sm0 = lds_addr(smem);
 
-  auto issue = [&](int t) {
-    uint8_t* buf = smem + (t % NPK) * PKT;
-    const int64_t tr0 = row0 + (int64_t)t * GRT;
-    if constexpr (P3) {
-      // row rr of the tile -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the row
+  // ---- LDS-DMA of tile t (piece i of PPW per wave).  A full tile's source is a uniform base plus a
+  // per-lane offset fixed for the kernel; only a chunk's last tile needs row clamping.
+  //   Phase III: tile row rr = 8w + i -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the
+  //              row; piece 8 = the tile's 32 f64 norms (every wave loads the same 256 B, so the DMA
+  //              count per wave is uniform).
+  //   Phase II:  rows 8w..8w+7 -> slot rr*8 + c' holding chunk c' ^ ((rr >> 1) & 7).
+  const int RB = P3 ? 1024 : 128;  // bytes per corpus row
+  uint32_t loff[P3 ? 8 : 1];
+  if constexpr (P3) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int rr = w * 8 + i;
-        int64_t row = tr0 + rr;
-        row = row < row1 ? row : row1 - 1;
-        __builtin_amdgcn_global_load_lds(src + row * 1024 + ((l ^ (rr & 15)) << 4),
-                                         (__attribute__((address_space(3))) void*)(buf + rr * 1024), 16, 0, 0);
+    for (int i = 0; i < 8; ++i) loff[i] = (uint32_t)(i * 1024 + ((l ^ ((8 * w + i) & 15)) << 4));
+  } else {
+    const int rr = 8 * w + (l >> 3);
+    loff[0] = (uint32_t)((l >> 3) * 128 + (((l & 7) ^ ((rr >> 1) & 7)) << 4));
+  }
+  auto issue_piece = [&](int t, int slot_i, int i) {
+    uint8_t* buf = smem + slot_i * PKT;
+    const int64_t tr0 = row0 + (int64_t)t * GRT;
+    const bool full = tr0 + GRT <= row1;
+    if (P3 && i == 8) {
+      const uint8_t* g = reinterpret_cast<const uint8_t*>(norms + tr0) + 4 * l;
+      if (!full) {
+        int64_t nr = tr0 + (l >> 1);
+        nr = nr < row1 ? nr : row1 - 1;
+        g = reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1);
       }
-      // the tile's 32 norms (every wave loads the same 256 B: equal DMA counts per wave)
-      int64_t nr = tr0 + (l >> 1);
-      nr = nr < row1 ? nr : row1 - 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1),
-                                       (__attribute__((address_space(3))) void*)(buf + T3), 4, 0, 0);
-    } else {
-      // rows 8w..8w+7: slot rr*8 + c' holds chunk c' ^ ((rr >> 1) & 7)
-      const int rr = 8 * w + (l >> 3), c = (l & 7) ^ ((rr >> 1) & 7);
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + T3), 4, 0, 0);
+      return;
+    }
+    const int ii = P3 ? i : 0;
+    const uint8_t* g = src + (tr0 + 8 * w) * RB + loff[ii];
+    if (!full) {  // the chunk's last tile: clamp rows past the end
+      const int rr = P3 ? 8 * w + i : 8 * w + (l >> 3);
       int64_t row = tr0 + rr;
       row = row < row1 ? row : row1 - 1;
-      __builtin_amdgcn_global_load_lds(src + row * 128 + c * 16,
-                                       (__attribute__((address_space(3))) void*)(buf + w * 1024), 16, 0, 0);
+      g = src + row * RB + (P3 ? ((l ^ (rr & 15)) << 4) : ((((l & 7) ^ ((rr >> 1) & 7))) << 4));
     }
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + (P3 ? (8 * w + i) * 1024 : w * 1024)),
+                                     16, 0, 0);
+  };
+  // Phase II expansion: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r, c = 2w + h
+  // (k-steps 4c..4c+3), and writes both lane halves' fragments of each ([k-step][lane][16 B])
+  const int uc = 2 * w + h;
+  const uint32_t usrc = (uint32_t)((r * 8 + (uc ^ ((r >> 1) & 7))) * 16);
+  auto unpack_frag = [&](const v4i& pv, int j, uint32_t ubw) {  // j = 2i + hh
+    const int i = j >> 1, hh = j & 1;
+    const uint32_t wd = (uint32_t)(i == 0 ? pv.x : i == 1 ? pv.y : i == 2 ? pv.z : pv.w);
+    v4i f;
+    f.x = (int)((wd >> (4 * hh + 0)) & 0x01010101u);
+    f.y = (int)((wd >> (4 * hh + 1)) & 0x01010101u);
+    f.z = (int)((wd >> (4 * hh + 2)) & 0x01010101u);
+    f.w = (int)((wd >> (4 * hh + 3)) & 0x01010101u);
+    lds_write128(ubw + (uint32_t)(((4 * uc + i) * 64 + hh * 32 + r) * 16), f);
   };
 
-  for (int t = 0; t < NPK - 1 && t < ntiles; ++t) issue(t);
+  for (int t = 0; t < AHEAD && t < ntiles; ++t)
+    static_for<0, PPW>([&](auto I) { issue_piece(t, t, decltype(I)::value); });
 
   // A fragments of this wave's 32 queries, both pieces, all 32 k-steps -> accumulator file
   const int qbase = qb * GQB + w * GQW;
-  v4i A[2][GKS];
+  v4i A[2][GKS];  // [piece] (two pieces) or [M-block] (one piece)
   {
-    const int8_t* qp = qa + (int64_t)(qbase + r) * QA_BYTES + h * 16;
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int j = 0; j < 2; ++j) {
+      const int8_t* qp = NPC == 2 ? qa + (int64_t)(qbase + r) * QA_BYTES + j * 1024 + h * 16
+                                  : qa + (int64_t)(qbase + 32 * j + r) * QA_BYTES + h * 16;
 #pragma unroll
-      for (int s = 0; s < GKS; ++s) A[p][s] = *reinterpret_cast<const v4i*>(qp + p * 1024 + s * 32);
+      for (int s = 0; s < GKS; ++s) A[j][s] = *reinterpret_cast<const v4i*>(qp + s * 32);
+    }
   }
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int s = 0; s < GKS; ++s) asm volatile("" : "+a"(A[p][s]));
-  float th[16];
+  // test e of a lane: M-block e >> 4, accumulator register g = e & 15 -> query row of the wave
+  auto qrow = [&](int e) { return 32 * (e >> 4) + ((e & 3) + 8 * ((e >> 2) & 3) + 4 * h); };
+  float th[NE];
 #pragma unroll
-  for (int g = 0; g < 16; ++g) th[g] = DENSE ? 0.f : thr[qbase + (g & 3) + 8 * (g >> 2) + 4 * h];
+  for (int e = 0; e < NE; ++e) th[e] = DENSE ? 0.f : thr[qbase + qrow(e)];
 
   // Phase III: B fragment of k-step s for lane (r, h) = 16-B chunk 2s+h of tile row r, at slot
   // r*64 + ((2s+h) ^ (r & 15)) = r*64 + 16*(s>>3) + off[s&7]
@@ -238,128 +303,150 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) boff[j] = (uint32_t)(((((2 * j) ^ (r & 14)) | (h ^ (r & 1))) << 4) + r * 1024);
 
+  const uint32_t lc0 = lds_addr(lcnt + w * GQW);
+  if (!DENSE && l < GQW) lcnt[w * GQW + l] = 0;  // made visible by the first tile's barrier
   v16i acc[2][2];        // [tile parity][piece]
-  float ures[16];        // u of the previous tile (flushed at the top of the next-but-one tile)
-  uint32_t hm = 0;       // hits of the previous tile: bit g = register g of this lane
+  float ures[NE];        // u of the previous tile (flushed at the top of the next-but-one tile)
+  uint64_t anyhit = 0;   // some lane's u >= thr in the previous tile (wave-uniform)
 #pragma unroll
-  for (int g = 0; g < 16; ++g) ures[g] = 0.f;
-  float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk); Phase II 0 / NaN
+  for (int e = 0; e < NE; ++e) ures[e] = 0.f;
+  float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
 
-  // u of register g from the accumulators of one tile; NaN for rows without a score
-  auto uval = [&](const v16i& a0, const v16i& a1, int g, float inv) {
-    const float u = fmaf((float)a1[g], 1.0f / 256.0f, (float)a0[g]);
-    return P3 ? u * inv : u + inv;  // Phase II: inv is 0 (valid) or NaN
+  // u of test e from the accumulators of one tile (Phase III: NaN for rows without a score)
+  auto uval = [&](const v16i& a0, const v16i& a1, int e, float inv) {
+    const int g = e & 15;
+    const float u = NPC == 2 ? fmaf((float)a1[g], 1.0f / 256.0f, (float)a0[g]) : (float)((e >> 4) ? a1[g] : a0[g]);
+    return P3 ? u * inv : u;
   };
   // results of tile tt (computed in the following tile's shadow) -> HBM
   auto flush = [&](int tt) {
     const int lr = tt * GRT + r;
     if constexpr (DENSE) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int q = qbase + (g & 3) + 8 * (g >> 2) + 4 * h;
-        if (q < nq && lr < nrows) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[g];
+      for (int e = 0; e < NE; ++e) {
+        const int q = qbase + qrow(e);
+        if (q < nq && lr < nrows) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[e];
       }
     } else {
-      if (__ballot(hm != 0)) {  // rare: ~k * n / sample rows per query over the corpus
-        uint32_t m = hm;
+      if (anyhit) {  // rare: ~k * n / sample rows per query over the corpus
+        uint32_t m = 0;
+        static_for<0, NE>([&](auto E) {
+          constexpr int e = decltype(E)::value;
+          m |= (ures[e] >= th[e] ? 1u : 0u) << e;
+        });
+        if (lr >= nrows) m = 0;
         while (m) {
-          const int g = __builtin_ctz(m);
+          const int e = __builtin_ctz(m);
           m &= m - 1;
-          const int q = qbase + (g & 3) + 8 * (g >> 2) + 4 * h;
-          const int pos = atomicAdd(ccnt + (int64_t)q * nchunks + chunk, 1);
-          if (pos < capc) cand[(int64_t)q * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + lr);
+          const int ql = qrow(e);  // list position from this wave's LDS counter
+          int pos;
+          lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+          if (pos < capc) cand[(int64_t)(qbase + ql) * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + lr);
         }
-        hm = 0;
+        anyhit = 0;
       }
     }
   };
+  auto test = [&](float u, int e) {
+    ures[e] = u;
+    if constexpr (!DENSE) anyhit |= __ballot(u >= th[e]);
+  };
 
+  if constexpr (!P3) {  // expand tile 0 before the loop (tile t+1 is expanded during tile t)
+    wait_vm<0>();
+    barrier_all();
+    v4i pv;
+    lds_read128(pv, sm0 + usrc);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv)::"memory");
+#pragma unroll
+    for (int j = 0; j < 8; ++j) unpack_frag(pv, j, sm0 + (uint32_t)(NP * T2));
+    wait_lgkm0();
+  }
+
+  int sl = 0;  // t % NP
   auto tile = [&](auto PAR, int t) {
     constexpr int p = decltype(PAR)::value;
-    // this wave's DMA of tile t landed (only tile t+1's may be outstanding; older stores too);
-    // after the barrier every wave's has, and every wave is done reading tile t-1's buffers
-    if (t + 1 < ntiles)
+    // Phase III: this wave's DMA of tile t landed (only tile t+1's may still be in flight; the
+    // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
+    // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
+    // the slots the DMA of this tile overwrites.
+    if (t + AHEAD - 1 < ntiles)
       wait_vm<PPW>();
     else
       wait_vm<0>();
-    barrier_all();
+    if (!(VRQ_G5_BISECT & 4)) barrier_all();
     if (t >= 2) flush(t - 2);
-    if (t + NPK - 1 < ntiles) issue(t + NPK - 1);  // into the slot of tile t-1
-    const uint32_t slot = sm0 + (uint32_t)((t % NPK) * PKT);
-    uint32_t bb;
+    const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
+    const bool dma = t + AHEAD < ntiles;
+    const int sla = sl == 0 ? NP - 1 : sl - 1;                       // (t + AHEAD) % NP = (t - 1) % NP
+    const int sl1 = sl + 1 == NP ? 0 : sl + 1;                       // (t + 1) % NP
+    double nv = 0.0;
+    v4i pv = {};
+    const uint32_t ubn = sm0 + (uint32_t)(NP * T2 + ((t + 1) & 1) * U2);  // Phase II: tile t+1 expanded here
+    uint32_t badr[8];
     if constexpr (P3) {
-      double nv;
       lds_read64(nv, slot + T3 + (uint32_t)(r * 8));
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nv)::"memory");
-      invc = (nv > 0.0 && t * GRT + r < nrows) ? (float)(1.0 / nv) : __builtin_nanf("");
-      bb = slot;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
     } else {
-      invc = (t * GRT + r < nrows) ? 0.f : __builtin_nanf("");
-      // expand the packed tile: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r,
-      // c = 2w + h (k-steps 4c..4c+3) and writes both lane halves' fragments of each
-      const int c = 2 * w + h;
-      v4i pv;
-      lds_read128(pv, slot + (uint32_t)((r * 8 + (c ^ ((r >> 1) & 7))) * 16));
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv)::"memory");
-      const uint32_t ubw = sm0 + (uint32_t)(NPK * T2 + (t & 1) * U2);
-      const uint32_t wd[4] = {(uint32_t)pv.x, (uint32_t)pv.y, (uint32_t)pv.z, (uint32_t)pv.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int s = 4 * c + i;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          v4i f;
-          f.x = (int)((wd[i] >> (4 * hh + 0)) & 0x01010101u);
-          f.y = (int)((wd[i] >> (4 * hh + 1)) & 0x01010101u);
-          f.z = (int)((wd[i] >> (4 * hh + 2)) & 0x01010101u);
-          f.w = (int)((wd[i] >> (4 * hh + 3)) & 0x01010101u);
-          lds_write128(ubw + (uint32_t)((s * 64 + hh * 32 + r) * 16), f);
-        }
-      }
-      wait_lgkm0();
-      barrier_all();
-      bb = ubw + (uint32_t)(l * 16);
+      badr[0] = sm0 + (uint32_t)(NP * T2 + (t & 1) * U2 + l * 16);
     }
-    v4i ring[4];
+    constexpr int BA = VRQ_G5_BAHEAD;                 // B fragments read BA k-steps ahead
+    constexpr int NR = BA < 4 ? 4 : 8;                // ring (power of two > BA)
+    v4i ring[NR];
     auto readB = [&](auto S) {
       constexpr int s = decltype(S)::value;
       if constexpr (P3)
-        lds_read128_off<(s >> 3) * 256>(ring[s & 3], bb + boff[s & 7]);
+        lds_read128_off<(s >> 3) * 256>(ring[s & (NR - 1)], badr[s & 7]);
       else
-        lds_read128_off<s * 1024>(ring[s & 3], bb);
+        lds_read128_off<s * 1024>(ring[s & (NR - 1)], badr[0]);
     };
-    readB(std::integral_constant<int, 0>{});
-    readB(std::integral_constant<int, 1>{});
+    static_for<0, BA>([&](auto S) { readB(S); });
     VRQ_SCHED_FENCE();
     static_for<0, GKS>([&](auto S) {
       constexpr int s = decltype(S)::value;
-      if constexpr (s + 2 < GKS) {
-        readB(std::integral_constant<int, s + 2>{});
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ring[s & 3])::"memory");
-      } else if constexpr (s + 1 < GKS) {
-        asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(ring[s & 3])::"memory");
+      if constexpr (s + BA < GKS) {
+        readB(std::integral_constant<int, s + BA>{});
+        // everything but the BA newest LDS operations is complete: B(s), and the norm (issued
+        // before B(0)) / the packed Phase-II tile (issued in step 1, before B(1 + BA))
+        asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(ring[s & (NR - 1)]), "+v"(nv), "+v"(pv) : "n"(BA) : "memory");
       } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ring[s & 3])::"memory");
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(GKS - 1 - s) : "memory");
       }
-      acc[p][0] = mfma_i8(A[0][s], ring[s & 3], s == 0 ? zero : acc[p][0]);
-      acc[p][1] = mfma_i8(A[1][s], ring[s & 3], s == 0 ? zero : acc[p][1]);
+      if constexpr (!(VRQ_G5_BISECT & 8)) {
+        acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
+        acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
+      } else if constexpr (s == 0) {
+        acc[p][0] = ring[0].x + zero;
+        acc[p][1] = ring[0].y + zero;
+      }
       asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
-      // threshold test / dense value of tile t-1, one register per k-step in 4..19
-      if constexpr (s >= 4 && s < 20) {
-        constexpr int g = s - 4;
-        if (t > 0) {
-          const float u = uval(acc[p ^ 1][0], acc[p ^ 1][1], g, invp);
-          if constexpr (DENSE)
-            ures[g] = u;
-          else
-            hm |= (u >= th[g] ? 1u : 0u) << g;
-        }
+      // DMA of tile t + AHEAD, spread over the MFMA shadow
+      if constexpr (P3) {
+        if constexpr (s >= 2 && s < 2 + 3 * 9 && (s - 2) % 3 == 0 && !(VRQ_G5_BISECT & 2))
+          if (dma) issue_piece(t + AHEAD, sla, (s - 2) / 3);
+      } else {
+        if constexpr (s == 2 && !(VRQ_G5_BISECT & 2))
+          if (dma) issue_piece(t + AHEAD, sla, 0);
+        if constexpr (s == 1) lds_read128(pv, sm0 + (uint32_t)(sl1 * T2) + usrc);
+        if constexpr (s >= 5 && s < 13) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
+      }
+      // threshold test / dense value of tile t-1, one per k-step in [EOFF, EOFF + NE)
+      constexpr int EOFF = NE == 16 ? 4 : 0;
+      if constexpr (s >= EOFF && s < EOFF + NE) {
+        constexpr int e = s - EOFF;
+        if (t > 0 && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e);
+      }
+      if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
+        invc = (nv > 0.0 && t * GRT + r < nrows) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
       }
       VRQ_SCHED_FENCE();
     });
     invp = invc;
+    sl = sl1;
   };
 
   int t = 0;
@@ -373,14 +460,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   if (ntiles >= 2) flush(ntiles - 2);
   const int pl = (ntiles - 1) & 1;
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
-    const float u = pl ? uval(acc[1][0], acc[1][1], g, invp) : uval(acc[0][0], acc[0][1], g, invp);
-    if constexpr (DENSE)
-      ures[g] = u;
-    else
-      hm |= (u >= th[g] ? 1u : 0u) << g;
-  }
+  for (int e = 0; e < NE; ++e)
+    test(pl ? uval(acc[1][0], acc[1][1], e, invp) : uval(acc[0][0], acc[0][1], e, invp), e);
   flush(ntiles - 1);
+  if constexpr (!DENSE) {
+    wait_lgkm0();
+    if (l < GQW && qbase + l < nq) ccnt[(int64_t)(qbase + l) * nchunks + chunk] = lcnt[w * GQW + l];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -535,6 +621,9 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restr
   __syncthreads();
   const int total = sh.misc[0];
   const int need = (int)((int64_t)k < n ? k : n);
+#ifdef VRQ_G5_DEBUG
+  if (tid == 0 && q < 8) printf("q %d candidates %d overflow %d capc %d\n", q, total, sh.misc[1], capc);
+#endif
   if (sh.misc[1] || total > FIN_CAP || total < need) {
     if (tid == 0) fb_flag[q] = 1;
     return;
@@ -641,8 +730,9 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   p->nqb = (nq + GQB - 1) / GQB;
   p->nq_pad = p->nqb * GQB;
   const int want = 256 / p->nqb > 0 ? 256 / p->nqb : 1;  // chunks per query block: one WG per CU
-  // sample rows: expected candidates k * n / S ~ FIN_CAP / 4 (VRQ_GEMM_SAMPLE_DIV overrides n / S)
-  int64_t S = (int64_t)(4.0 * (double)k * (double)n / (double)FIN_CAP);
+  // sample rows: the sampled threshold alone admits ~k * n / S rows per query; aim at FIN_CAP /
+  // CAP_MULT so that the margin's extra rows still fit (VRQ_GEMM_SAMPLE_DIV overrides n / S)
+  int64_t S = (int64_t)((double)CAP_MULT * (double)k * (double)n / (double)FIN_CAP);
   const char* ev = getenv("VRQ_GEMM_SAMPLE_DIV");
   if (ev && atoi(ev) >= 1) S = n / atoi(ev);
   if (S < kMinSample) S = kMinSample;
@@ -662,7 +752,7 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   const int64_t Sv = S < n ? S : n;
   const int64_t expect = ((int64_t)k * cr + Sv - 1) / Sv;
   int capc = 64;
-  while (capc < 4 * expect && capc < 4096) capc <<= 1;
+  while (capc < CAP_MULT * expect && capc < 4096) capc <<= 1;
   p->capc = capc;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t qa = al((size_t)p->nq_pad * QA_BYTES);
@@ -681,6 +771,8 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
 
 using namespace vrq;
 using namespace vrq::g5;
+
+extern "C" int vrq_gemm_topk_pieces(void) { return NPC; }
 
 extern "C" size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k) {
   GemmPlan p;
