@@ -15,6 +15,13 @@ def short(name):
     if "hamming_mfma" in name:  # template MODE: 0 thresholded pass, 1 dense sample pass, 2 re-run
         return {"1": "hamming_mfma_kernel_sample", "2": "hamming_mfma_kernel_rerun"}.get(
             name.split("hamming_mfma_kernel<", 1)[-1][:1], "hamming_mfma_kernel")
+    if "gemm_topk_kernel" in name:  # <PH, DENSE>: PH 3 = int8 cosine, 2 = binary
+        t = name.split("gemm_topk_kernel<", 1)[-1]
+        base = "gemm_topk_kernel" if t.startswith("3") else "gemm_topk_kernel_binary"
+        return base + ("_sample" if "true" in t.split(">")[0] else "")
+    for nm in ("gemm_select_kernel", "gemm_finish_kernel", "gemm_fallback_kernel", "gemm_prep_kernel"):
+        if nm in name:
+            return nm + ("_binary" if "<2>" in name else "")
     if "sample_select" in name:
         return "sample_select_kernel"
     if "sample_check" in name:
@@ -47,7 +54,7 @@ def main(src, dst, tag):
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         out["kernel_stats"] = [r for r in csv.DictReader(open(stats[0]))]
-    for name in ("pmc_sq", "pmc_mfma", "pmc_fetch", "pmc_write"):
+    for name in ("pmc_sq", "pmc_mfma", "pmc_v", "pmc_fetch", "pmc_write"):
         f = glob.glob(os.path.join(src, name, "*counter_collection.csv"))
         if f:
             out[name] = pmc(f[0])

@@ -49,6 +49,9 @@
 #ifndef VRQ_G5_BAHEAD
 #define VRQ_G5_BAHEAD 2
 #endif
+#ifndef VRQ_G5_NP3
+#define VRQ_G5_NP3 3
+#endif
 #ifndef VRQ_G5_PIECES
 #define VRQ_G5_PIECES 1
 #endif
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
   // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
   // packed tile t+1 expanded into the unpacked ring (2 tiles) during tile t.
-  constexpr int NP = P3 ? 3 : 4;
+  constexpr int NP = P3 ? VRQ_G5_NP3 : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
   constexpr int PPW = P3 ? 9 : 1;                     // LDS-DMA instructions per wave per tile
@@ -373,10 +376,14 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
     // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
     // the slots the DMA of this tile overwrites.
-    if (t + AHEAD - 1 < ntiles)
-      wait_vm<PPW>();
-    else
-      wait_vm<0>();
+    {  // the DMA of the tile needed now (t; Phase II: t+1) landed; the INF tiles issued after it may
+       // stay in flight (in the chunk's last tiles: wait for everything)
+      constexpr int NEED = P3 ? 0 : 1, INF = AHEAD - 1 - NEED;
+      if (t + NEED + INF < ntiles)
+        wait_vm<INF * PPW>();
+      else
+        wait_vm<0>();
+    }
     if (!(VRQ_G5_BISECT & 4)) barrier_all();
     if (t >= 2) flush(t - 2);
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
@@ -729,7 +736,11 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   if (n < 1 || n >= (int64_t(1) << 32) || nq < 1 || k < 1 || k > KMAX5) return VRQ_EUNSUPPORTED;
   p->nqb = (nq + GQB - 1) / GQB;
   p->nq_pad = p->nqb * GQB;
-  const int want = 256 / p->nqb > 0 ? 256 / p->nqb : 1;  // chunks per query block: one WG per CU
+  // chunks per query block: one WG per CU (x VRQ_GEMM_CHUNK_MULT, a tuning override: shorter chunks
+  // keep the query blocks that share a chunk closer in time, so they share its L2 lines)
+  const char* cm = getenv("VRQ_GEMM_CHUNK_MULT");
+  const int mult = cm && atoi(cm) >= 1 ? atoi(cm) : 1;
+  const int want = (256 / p->nqb > 0 ? 256 / p->nqb : 1) * mult;
   // sample rows: the sampled threshold alone admits ~k * n / S rows per query; aim at FIN_CAP /
   // CAP_MULT so that the margin's extra rows still fit (VRQ_GEMM_SAMPLE_DIV overrides n / S)
   int64_t S = (int64_t)((double)CAP_MULT * (double)k * (double)n / (double)FIN_CAP);
