@@ -41,6 +41,10 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 __device__ __forceinline__ void lds_read128(v4i& d, uint32_t a) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
+template <int OFF>
+__device__ __forceinline__ void lds_read128_imm(v4i& d, uint32_t a) {  // address + immediate offset
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
 __device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
