@@ -214,15 +214,22 @@ def exhaustive_scores(mode: str, qf: np.ndarray, codes: np.ndarray = None, x8: n
     GPU's definition; NumPy's sdot is within a few ulps of it).
     """
     q64 = np.asarray(qf, dtype=np.float32).astype(np.float64)
-    if mode == "binary":
-        pm = (2 * np.unpackbits(codes, axis=1).astype(np.int8) - 1).astype(np.float64)
-        return q64 @ pm.T
-    dot = (q64 @ np.asarray(x8).astype(np.float64).T).astype(np.float32).astype(np.float64)
-    nrm = int8_row_norms(x8)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        s = dot / nrm[None, :]
-    s[:, nrm == 0] = -np.inf
-    return s
+    n = (codes if mode == "binary" else x8).shape[0]
+    out = np.empty((q64.shape[0], n), dtype=np.float64)
+    for a in range(0, n, 16384):                      # row blocks: bounded host memory
+        b = min(n, a + 16384)
+        if mode == "binary":
+            pm = (2 * np.unpackbits(codes[a:b], axis=1).astype(np.int8) - 1).astype(np.float64)
+            out[:, a:b] = q64 @ pm.T
+            continue
+        xb = np.asarray(x8[a:b])
+        dot = (q64 @ xb.astype(np.float64).T).astype(np.float32).astype(np.float64)
+        nrm = int8_row_norms(xb)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            sb = dot / nrm[None, :]
+        sb[:, nrm == 0] = -np.inf
+        out[:, a:b] = sb
+    return out
 
 
 def exhaustive_topk(scores: np.ndarray, k: int):

@@ -144,3 +144,18 @@ def test_gemm_topk_stage_split(dev):
     torch.cuda.synchronize()
     for a, b in zip(full, part):
         assert torch.equal(a, b)
+
+
+def test_gemm_topk_many_candidates(dev, monkeypatch):
+    """A small sample (VRQ_GEMM_SAMPLE_DIV) and k = 100 leave thousands of candidates per query: the
+    finish kernel's running top-k walks them in several batches; the fallback stays off."""
+    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")
+    monkeypatch.setenv("VRQ_GEMM_SAMPLE_DIV", "8")
+    rng = np.random.default_rng(17)
+    n, nq, k = 200_000, 40, 100
+    F = _corpus(rng, n, 32)
+    codes, x8, _ = O.encode_batch("cohere", F, 0.1)
+    qf = _queries(rng, F, nq)
+    for mode in ("binary", "int8_cosine"):
+        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8)
+        _check(mode, qf, k, cnt, rows, sc, codes=codes, x8=x8)

@@ -21,9 +21,9 @@
 //     rows have s' >= U - Delta, so every row of the exact top-k -- ties with the k-th included --
 //     has u >= thr.
 //  4. main pass: every row with u >= thr is appended to a per-(query, chunk) candidate list.
-//  5. finish: exact reference scores of the candidates, sort by (s desc, row asc), first k.  A list
-//     overflow, more than FIN_CAP candidates, or fewer than min(k, n) of them (zero-norm rows,
-//     heavy ties) sends the query to the exact fallback: one workgroup scans every row.
+//  5. finish: exact reference scores of the candidates, running top-k by (s desc, row asc).  A list
+//     overflow (heavy ties) or fewer than min(k, n) candidates (zero-norm rows) sends the query to
+//     the exact fallback: one workgroup scans every row.
 //
 // Work decomposition of the two matrix passes: one 256-thread workgroup per CU; each wave holds the
 // int8 piece of 64 queries (two pieces of 32) for all of d = 1024 in the accumulator file (256 AGPRs);
@@ -52,6 +52,9 @@
 #ifndef VRQ_G5_NP3
 #define VRQ_G5_NP3 3
 #endif
+#ifndef VRQ_G5_DMA_STRIDE
+#define VRQ_G5_DMA_STRIDE 3  // k-steps between the LDS-DMA pieces of the next-but-one tile
+#endif
 #ifndef VRQ_G5_PIECES
 #define VRQ_G5_PIECES 1
 #endif
@@ -70,8 +73,9 @@ constexpr int NMB = 3 - NPC;         // 32-query M-blocks per wave
 constexpr int GQW = 32 * NMB;        // queries per wave
 constexpr int GQB = GW * GQW;        // queries per workgroup
 constexpr int NE = 16 * NMB;         // threshold tests per lane per tile
-// candidates sorted in LDS per query by the finish kernel, and the per-(query, chunk) list capacity
-// as a multiple of the hits the sample predicts (one piece: ~4x wider margin)
+// planning target for the candidates per query (the sample size follows from it), and the
+// per-(query, chunk) list capacity as a multiple of the hits the sample predicts (one piece: ~4x
+// wider margin)
 constexpr int FIN_CAP = NPC == 2 ? 4096 : 8192;
 constexpr int CAP_MULT = NPC == 2 ? 4 : 16;
 constexpr int GRT = 32;              // corpus rows per tile (one 32-column N-block)
@@ -433,8 +437,9 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
       // DMA of tile t + AHEAD, spread over the MFMA shadow
       if constexpr (P3) {
-        if constexpr (s >= 2 && s < 2 + 3 * 9 && (s - 2) % 3 == 0 && !(VRQ_G5_BISECT & 2))
-          if (dma) issue_piece(t + AHEAD, sla, (s - 2) / 3);
+        constexpr int DS = VRQ_G5_DMA_STRIDE;
+        if constexpr (s >= 2 && s < 2 + DS * 9 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2))
+          if (dma) issue_piece(t + AHEAD, sla, (s - 2) / DS);
       } else {
         if constexpr (s == 2 && !(VRQ_G5_BISECT & 2))
           if (dma) issue_piece(t + AHEAD, sla, 0);
@@ -592,14 +597,61 @@ __device__ __forceinline__ double exact_score(const float (&qv)[DPL], const uint
     return phase3_cos(qv, x8 + row * DIM, norms[row]);
 }
 
+// Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
+// exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
+// (score desc, row asc), so the sort runs rarely once the list is full.  key/row[0..kc) hold the
+// running list in order.  All threads of the block call it; returns kc = min(k, count).
+template <int PH, class RowAt>
+__device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const uint8_t* codes,
+                            const int8_t* x8, const double* norms, int k, uint64_t* key, uint32_t* row,
+                            int32_t* fill) {
+  const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  if (tid == 0) *fill = 0;
+  int kc = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < count; base += FB_BATCH) {
+    const uint64_t kk = kc == k ? key[k - 1] : KEY_NONE;
+    const uint32_t kr = kc == k ? row[k - 1] : 0xffffffffu;
+    const int64_t end = base + FB_BATCH < count ? base + FB_BATCH : count;
+    for (int64_t j = base + w; j < end; j += 4) {
+      const uint32_t rr = row_at(j);
+      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, codes, x8, norms, (int64_t)rr));
+      const bool take = kc < k || key_r < kk || (key_r == kk && rr < kr);
+      if (take && l == 0) {
+        const int i = kc + atomicAdd(fill, 1);
+        key[i] = key_r;
+        row[i] = rr;
+      }
+    }
+    __syncthreads();
+    const int f = *fill;
+    if (f > 0) {
+      const int tot = kc + f;
+      const int np2 = next_pow2(tot);
+      for (int i = tot + tid; i < np2; i += 256) {
+        key[i] = KEY_NONE;
+        row[i] = 0xffffffffu;
+      }
+      block_sort_pairs(key, row, np2);
+      kc = tot < k ? tot : k;
+    }
+    if (tid == 0) *fill = 0;
+    __syncthreads();
+  }
+  return kc;
+}
+
+constexpr int MAX_CHUNKS = 2048;  // per-query candidate lists the finish kernel indexes
 struct FinShared {
-  uint64_t key[FIN_CAP];
-  uint32_t row[FIN_CAP];
+  uint64_t key[KMAX5 + FB_BATCH];
+  uint32_t row[KMAX5 + FB_BATCH];
+  int32_t pre[MAX_CHUNKS + 1];  // exclusive prefix of the list lengths
   int32_t misc[4];
 };
 
-// finish: candidates of the query -> exact scores -> sorted -> first min(k, n).  Flags the query for
-// the fallback instead when the candidates cannot be trusted to hold the top-k.
+// finish: the query's candidate lists -> exact scores -> running top-k -> first min(k, n).  A list
+// overflow (rows the main pass could not record) or fewer than min(k, n) candidates (zero-norm rows)
+// flags the query for the fallback instead.
 template <int PH>
 __global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restrict__ codes,
                                                           const int8_t* __restrict__ x8,
@@ -612,61 +664,60 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restr
                                                           double* __restrict__ out_scores,
                                                           int32_t* __restrict__ fb_flag) {
   __shared__ FinShared sh;
-  const int q = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = tid >> 6;
-  if (tid == 0) {
-    sh.misc[0] = 0;  // total
-    sh.misc[1] = 0;  // overflow
-    sh.misc[2] = 0;  // fill
-  }
+  const int q = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) sh.misc[1] = 0;  // overflow
   __syncthreads();
   const int32_t* cq = ccnt + (int64_t)q * nchunks;
-  for (int c = tid; c < nchunks; c += 256) {
-    const int v = cq[c];
-    atomicAdd(&sh.misc[0], v < capc ? v : capc);
-    if (v > capc) atomicOr(&sh.misc[1], 1);
+  for (int c = tid; c < nchunks; c += 256)
+    if (cq[c] > capc) atomicOr(&sh.misc[1], 1);
+  if (tid == 0) {
+    int acc = 0;
+    for (int c = 0; c < nchunks; ++c) {
+      sh.pre[c] = acc;
+      const int v = cq[c];
+      acc += v < capc ? v : capc;
+    }
+    sh.pre[nchunks] = acc;
   }
   __syncthreads();
-  const int total = sh.misc[0];
+  const int total = sh.pre[nchunks];
   const int need = (int)((int64_t)k < n ? k : n);
 #ifdef VRQ_G5_DEBUG
-  if (tid == 0 && q < 8) printf("q %d candidates %d overflow %d capc %d\n", q, total, sh.misc[1], capc);
+  if (tid == 0 && (sh.misc[1] || total < need || q < 4))
+    printf("q %d candidates %d overflow %d capc %d\n", q, total, sh.misc[1], capc);
 #endif
-  if (sh.misc[1] || total > FIN_CAP || total < need) {
+  if (sh.misc[1] || total < need) {
     if (tid == 0) fb_flag[q] = 1;
     return;
   }
   const uint32_t* Cq = cand + (int64_t)q * nchunks * capc;
-  for (int c = 0; c < nchunks; ++c) {
-    const int v = cq[c];
-    for (int i = tid; i < v; i += 256) sh.row[atomicAdd(&sh.misc[2], 1)] = Cq[(int64_t)c * capc + i];
-  }
-  __syncthreads();
+  auto row_at = [&](int64_t j) {  // candidate j of the concatenated lists (binary search by chunk)
+    int lo = 0, hi = nchunks - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sh.pre[mid] <= j)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    return Cq[(int64_t)lo * capc + (j - sh.pre[lo])];
+  };
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  for (int i = w; i < total; i += 4) {
-    const double s = exact_score<PH>(qv, codes, x8, norms, (int64_t)sh.row[i]);
-    if (l == 0) sh.key[i] = desc_key_f64(s);
-  }
-  const int np2 = next_pow2(total > 1 ? total : 1);
-  for (int i = total + tid; i < np2; i += 256) {
-    sh.key[i] = KEY_NONE;
-    sh.row[i] = 0xffffffffu;
-  }
-  __syncthreads();
-  block_sort_pairs(sh.key, sh.row, np2);
+  const int kc = running_topk<PH>(total, row_at, qv, codes, x8, norms, k, sh.key, sh.row, &sh.misc[2]);
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
-    out_rows[o] = i < need ? (int64_t)sh.row[i] + row_offset : -1;
-    out_scores[o] = i < need ? desc_key_inv(sh.key[i]) : __builtin_nan("");
+    out_rows[o] = i < kc ? (int64_t)sh.row[i] + row_offset : -1;
+    out_scores[o] = i < kc ? desc_key_inv(sh.key[i]) : __builtin_nan("");
   }
   if (tid == 0) {
-    out_count[q] = need;
+    out_count[q] = kc;
     fb_flag[q] = 0;
   }
 }
 
-// fallback: exact running top-k over every row for the flagged queries (heavy ties, zero-norm rows,
-// list overflow).  One workgroup per query; rows enter the sort only when they beat the current k-th.
+// fallback: exact running top-k over every row for the flagged queries (list overflow from heavy
+// ties, zero-norm rows).  One workgroup per flagged query.
 template <int PH>
 __global__ __launch_bounds__(256) void gemm_fallback_kernel(const uint8_t* __restrict__ codes,
                                                             const int8_t* __restrict__ x8,
@@ -679,41 +730,12 @@ __global__ __launch_bounds__(256) void gemm_fallback_kernel(const uint8_t* __res
   __shared__ uint64_t key[KMAX5 + FB_BATCH];
   __shared__ uint32_t row[KMAX5 + FB_BATCH];
   __shared__ int32_t fill;
-  const int q = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  const int q = blockIdx.x, tid = threadIdx.x;
   if (!fb_flag[q]) return;
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  if (tid == 0) fill = 0;
-  int kc = 0;  // entries of the running top list key[0..kc)
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += FB_BATCH) {
-    const uint64_t kk = kc == k ? key[k - 1] : KEY_NONE;
-    const uint32_t kr = kc == k ? row[k - 1] : 0xffffffffu;
-    const int64_t end = base + FB_BATCH < n ? base + FB_BATCH : n;
-    for (int64_t rr = base + w; rr < end; rr += 4) {
-      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, codes, x8, norms, rr));
-      const bool take = kc < k || key_r < kk || (key_r == kk && (uint32_t)rr < kr);
-      if (take && l == 0) {
-        const int i = kc + atomicAdd(&fill, 1);
-        key[i] = key_r;
-        row[i] = (uint32_t)rr;
-      }
-    }
-    __syncthreads();
-    const int f = fill;
-    if (f > 0) {
-      const int tot = kc + f;
-      const int np2 = next_pow2(tot);
-      for (int i = tot + tid; i < np2; i += 256) {
-        key[i] = KEY_NONE;
-        row[i] = 0xffffffffu;
-      }
-      block_sort_pairs(key, row, np2);
-      kc = tot < k ? tot : k;
-    }
-    if (tid == 0) fill = 0;
-    __syncthreads();
-  }
+  const int kc =
+      running_topk<PH>(n, [](int64_t j) { return (uint32_t)j; }, qv, codes, x8, norms, k, key, row, &fill);
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)row[i] + row_offset : -1;
@@ -758,6 +780,7 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   p->scols = nsc * scr;
   int64_t cr = (n + want - 1) / want;
   cr = (cr + GRT - 1) / GRT * GRT;
+  if ((n + cr - 1) / cr > MAX_CHUNKS) cr = ((n + MAX_CHUNKS - 1) / MAX_CHUNKS + GRT - 1) / GRT * GRT;
   p->chunk_rows = cr;
   p->nchunks = (int)((n + cr - 1) / cr);
   const int64_t Sv = S < n ? S : n;
