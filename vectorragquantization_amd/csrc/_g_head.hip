@@ -224,16 +224,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   const int ntiles = (nrows + GRT - 1) / GRT;
   const uint32_t sm0 = lds_addr(smem);
 
-  // ---- Tiles: tile t covers chunk rows [tstart(t), tstart(t) + 32).  The last tile of a chunk whose
-  // length is not a multiple of 32 is shifted back to end at the chunk's end; its first rows (already
-  // in the previous tile) are masked out, so every DMA reads a whole, in-bounds 32-row tile.  Only a
-  // chunk shorter than 32 rows (tiny corpus) clamps rows instead.
-  const bool tiny = nrows < GRT;
-  auto tstart = [&](int t) { return tiny ? 0 : (t * GRT < nrows - GRT ? t * GRT : nrows - GRT); };
-  auto lane_valid = [&](int t) {  // this lane's tile row r holds a row of tile t not seen before
-    return tiny ? r < nrows : r >= t * GRT - tstart(t);
-  };
-  // ---- LDS-DMA of tile t (piece i of PPW per wave): a uniform base plus a per-lane offset.
+  // ---- LDS-DMA of tile t (piece i of PPW per wave).  A full tile's source is a uniform base plus a
+  // per-lane offset fixed for the kernel; only a chunk's last tile needs row clamping.
   //   Phase III: tile row rr = 8w + i -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the
   //              row; piece 8 = the tile's 32 f64 norms (every wave loads the same 256 B, so the DMA
   //              count per wave is uniform).
@@ -247,33 +239,29 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     const int rr = 8 * w + (l >> 3);
     loff[0] = (uint32_t)((l >> 3) * 128 + (((l & 7) ^ ((rr >> 1) & 7)) << 4));
   }
-  auto issue_piece = [&](int t, int slot_i, int i) {  // whole tiles (not tiny)
+  auto issue_piece = [&](int t, int slot_i, int i) {
     uint8_t* buf = smem + slot_i * PKT;
-    const int64_t tr0 = row0 + tstart(t);
+    const int64_t tr0 = row0 + (int64_t)t * GRT;
+    const bool full = tr0 + GRT <= row1;
     if (P3 && i == 8) {
-      // (pointer arguments through locals: a compound expression here makes the host-side compile
-      // silently drop the kernel's launch stub)
       const uint8_t* g = reinterpret_cast<const uint8_t*>(norms + tr0) + 4 * l;
+      if (!full) {
+        int64_t nr = tr0 + (l >> 1);
+        nr = nr < row1 ? nr : row1 - 1;
+        g = reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1);
+      }
       __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + T3), 4, 0, 0);
       return;
     }
-    const uint8_t* g = src + (tr0 + 8 * w) * RB + loff[P3 ? i : 0];
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + (P3 ? (8 * w + i) * 1024 : w * 1024)),
-                                     16, 0, 0);
-  };
-  auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
-    if (P3 && i == 8) {
-      int64_t nr = row0 + (l >> 1);
-      nr = nr < row1 ? nr : row1 - 1;
-      const uint8_t* g = reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1);
-      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + T3), 4, 0, 0);
-      return;
+    const int ii = P3 ? i : 0;
+    const uint8_t* g = src + (tr0 + 8 * w) * RB + loff[ii];
+    if (!full) {  // the chunk's last tile: clamp rows past the end
+      const int rr = P3 ? 8 * w + i : 8 * w + (l >> 3);
+      int64_t row = tr0 + rr;
+      row = row < row1 ? row : row1 - 1;
+      g = src + row * RB + (P3 ? ((l ^ (rr & 15)) << 4) : ((((l & 7) ^ ((rr >> 1) & 7))) << 4));
     }
-    const int rr = P3 ? 8 * w + i : 8 * w + (l >> 3);
-    int64_t row = row0 + rr;
-    row = row < row1 ? row : row1 - 1;
-    const uint8_t* g = src + row * RB + (P3 ? ((l ^ (rr & 15)) << 4) : ((((l & 7) ^ ((rr >> 1) & 7))) << 4));
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + (P3 ? (8 * w + i) * 1024 : w * 1024)),
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + (P3 ? (8 * w + i) * 1024 : w * 1024)),
                                      16, 0, 0);
   };
   // Phase II expansion: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r, c = 2w + h
@@ -291,15 +279,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     lds_write128(ubw + (uint32_t)(((4 * uc + i) * 64 + hh * 32 + r) * 16), f);
   };
 
-  for (int t = 0; t < AHEAD && t < ntiles; ++t) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      if (tiny)
-        issue_tiny(i);
-      else
-        issue_piece(t, t, i);
-    }
-  }
+  for (int t = 0; t < AHEAD && t < ntiles; ++t)
+    static_for<0, PPW>([&](auto I) { issue_piece(t, t, decltype(I)::value); });
 
   // A fragments of this wave's 32 queries, both pieces, all 32 k-steps -> accumulator file
   const int qbase = qb * GQB + w * GQW;
@@ -332,44 +313,37 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   const uint32_t lc0 = lds_addr(lcnt + w * GQW);
   if (!DENSE && l < GQW) lcnt[w * GQW + l] = 0;  // made visible by the first tile's barrier
   v16i acc[2][2];        // [tile parity][piece]
-  // results of the previous tile (flushed at the top of the next-but-one tile): the sample pass
-  // keeps u; the thresholded pass keeps u - thr (a hit iff >= 0; NaN never) and their running max
-  float ures[NE];
-  float umax = -__builtin_inff();
+  float ures[NE];        // u of the previous tile (flushed at the top of the next-but-one tile)
+  uint64_t anyhit = 0;   // some lane's u >= thr in the previous tile (wave-uniform)
 #pragma unroll
   for (int e = 0; e < NE; ++e) ures[e] = 0.f;
   float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
 
-  // u of test e from the accumulators of one tile (Phase III: NaN for rows without a score), minus
-  // the query's threshold in the thresholded pass (one fma for Phase III)
+  // u of test e from the accumulators of one tile (Phase III: NaN for rows without a score)
   auto uval = [&](const v16i& a0, const v16i& a1, int e, float inv) {
     const int g = e & 15;
     const float u = NPC == 2 ? fmaf((float)a1[g], 1.0f / 256.0f, (float)a0[g]) : (float)((e >> 4) ? a1[g] : a0[g]);
-    if constexpr (DENSE)
-      return P3 ? u * inv : u;
-    else
-      return P3 ? fmaf(u, inv, -th[e]) : u - th[e];
+    return P3 ? u * inv : u;
   };
   // results of tile tt (computed in the following tile's shadow) -> HBM
   auto flush = [&](int tt) {
-    const int lr = tstart(tt) + r;
-    const bool ok = lane_valid(tt);
+    const int lr = tt * GRT + r;
     if constexpr (DENSE) {
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         const int q = qbase + qrow(e);
-        if (q < nq && ok) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[e];
+        if (q < nq && lr < nrows) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[e];
       }
     } else {
-      if (__ballot(umax >= 0.f)) {  // rare: ~k * n / sample rows per query over the corpus
+      if (anyhit) {  // rare: ~k * n / sample rows per query over the corpus
         uint32_t m = 0;
         static_for<0, NE>([&](auto E) {
           constexpr int e = decltype(E)::value;
-          m |= (ures[e] >= 0.f ? 1u : 0u) << e;
+          m |= (ures[e] >= th[e] ? 1u : 0u) << e;
         });
-        if (!ok) m = 0;
+        if (lr >= nrows) m = 0;
         while (m) {
           const int e = __builtin_ctz(m);
           m &= m - 1;
@@ -379,15 +353,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
           if (pos < capc) cand[(int64_t)(qbase + ql) * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + lr);
         }
+        anyhit = 0;
       }
-      umax = -__builtin_inff();
     }
   };
   auto test = [&](float u, int e) {
     ures[e] = u;
-    if constexpr (!DENSE) {  // pairs fold into one v_max3
-      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));
-    }
+    if constexpr (!DENSE) anyhit |= __ballot(u >= th[e]);
   };
 
   if constexpr (!P3) {  // expand tile 0 before the loop (tile t+1 is expanded during tile t)
@@ -402,9 +374,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   }
 
   int sl = 0;  // t % NP
-  auto tile = [&](auto PAR, auto FIRST, int t) {
+  auto tile = [&](auto PAR, int t) {
     constexpr int p = decltype(PAR)::value;
-    constexpr bool first = decltype(FIRST)::value;  // tile 0: no previous tile to test
     // Phase III: this wave's DMA of tile t landed (only tile t+1's may still be in flight; the
     // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
     // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
@@ -479,10 +450,10 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       constexpr int EOFF = NE == 16 ? 4 : 0;
       if constexpr (s >= EOFF && s < EOFF + NE) {
         constexpr int e = s - EOFF;
-        if constexpr (!first && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e);
+        if (t > 0 && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e);
       }
       if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
-        invc = (nv > 0.0 && lane_valid(t)) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
+        invc = (nv > 0.0 && t * GRT + r < nrows) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
       }
       VRQ_SCHED_FENCE();
     });
@@ -490,16 +461,12 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     sl = sl1;
   };
 
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using NOTFIRST = std::integral_constant<bool, false>;
-  tile(I0{}, std::integral_constant<bool, true>{}, 0);
-  int t = 1;
+  int t = 0;
   for (; t + 1 < ntiles; t += 2) {
-    tile(I1{}, NOTFIRST{}, t);
-    tile(I0{}, NOTFIRST{}, t + 1);
+    tile(std::integral_constant<int, 0>{}, t);
+    tile(std::integral_constant<int, 1>{}, t + 1);
   }
-  if (t < ntiles) tile(I1{}, NOTFIRST{}, t);
+  if (t < ntiles) tile(std::integral_constant<int, 0>{}, t);
   wait_vm<0>();
   // tile ntiles-2 (tested during the last tile), then the last tile itself
   if (ntiles >= 2) flush(ntiles - 2);
