@@ -247,19 +247,31 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     const int rr = 8 * w + (l >> 3);
     loff[0] = (uint32_t)((l >> 3) * 128 + (((l & 7) ^ ((rr >> 1) & 7)) << 4));
   }
-  auto issue_piece = [&](int t, int slot_i, int i) {  // whole tiles (not tiny)
-    uint8_t* buf = smem + slot_i * PKT;
+  // per-tile uniform DMA bases (computed once per tile, held in SGPRs); piece i adds lane offsets
+  struct DmaTile {
+    const uint8_t* gsrc;
+    const uint8_t* gnrm;
+    uint8_t* lds;
+  };
+  auto dma_tile = [&](int t, int slot_i) {  // whole tiles (not tiny)
     const int64_t tr0 = row0 + tstart(t);
+    DmaTile d;
+    d.gsrc = src + (tr0 + 8 * w) * RB;
+    d.gnrm = reinterpret_cast<const uint8_t*>(norms + tr0);
+    d.lds = smem + slot_i * PKT;
+    return d;
+  };
+  auto issue_piece = [&](const DmaTile& d, int i) {
+    // (pointer arguments through locals: a compound expression here makes the host-side compile
+    // silently drop the kernel's launch stub)
     if (P3 && i == 8) {
-      // (pointer arguments through locals: a compound expression here makes the host-side compile
-      // silently drop the kernel's launch stub)
-      const uint8_t* g = reinterpret_cast<const uint8_t*>(norms + tr0) + 4 * l;
-      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + T3), 4, 0, 0);
+      const uint8_t* g = d.gnrm + 4 * l;
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(d.lds + T3), 4, 0, 0);
       return;
     }
-    const uint8_t* g = src + (tr0 + 8 * w) * RB + loff[P3 ? i : 0];
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(buf + (P3 ? (8 * w + i) * 1024 : w * 1024)),
-                                     16, 0, 0);
+    const uint8_t* g = d.gsrc + loff[P3 ? i : 0];
+    uint8_t* ld = d.lds + (P3 ? (8 * w + i) * 1024 : w * 1024);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
     if (P3 && i == 8) {
@@ -297,7 +309,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       if (tiny)
         issue_tiny(i);
       else
-        issue_piece(t, t, i);
+        issue_piece(dma_tile(t, t), i);
     }
   }
 
@@ -421,7 +433,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     if (t >= 2) flush(t - 2);
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
     const bool dma = t + AHEAD < ntiles;
-    const int sla = sl == 0 ? NP - 1 : sl - 1;                       // (t + AHEAD) % NP = (t - 1) % NP
+    const DmaTile dt = dma_tile(dma ? t + AHEAD : t, sl == 0 ? NP - 1 : sl - 1);
     const int sl1 = sl + 1 == NP ? 0 : sl + 1;                       // (t + 1) % NP
     double nv = 0.0;
     v4i pv = {};
@@ -468,10 +480,10 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       if constexpr (P3) {
         constexpr int DS = VRQ_G5_DMA_STRIDE;
         if constexpr (s >= 2 && s < 2 + DS * 9 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2))
-          if (dma) issue_piece(t + AHEAD, sla, (s - 2) / DS);
+          if (dma) issue_piece(dt, (s - 2) / DS);
       } else {
         if constexpr (s == 2 && !(VRQ_G5_BISECT & 2))
-          if (dma) issue_piece(t + AHEAD, sla, 0);
+          if (dma) issue_piece(dt, 0);
         if constexpr (s == 1) lds_read128(pv, sm0 + (uint32_t)(sl1 * T2) + usrc);
         if constexpr (s >= 5 && s < 13) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
       }
