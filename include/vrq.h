@@ -179,6 +179,26 @@ int vrq_rescore_int8_cosine(const float* qf, int32_t nq, int32_t dim, const int8
 int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit, uint8_t* codes,
                void* q, double* minmax, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Search side of the VectorDB* classes: dequantisation and the
+ * dequantised-dot rescoring of Phase-I candidates.  mode is the VRQ_ENC_* mode that produced the
+ * codes (INT8_GLOBAL, INT16_GLOBAL, INT4_GLOBAL, INT8_LOCAL, INT4_LOCAL):
+ *   VectorDBInt8Global._dequantize_int8   VectorDBInt8Global.py:144-152
+ *   VectorDBInt16Global._dequantize_int16 VectorDBInt16Global.py:144-152
+ *   VectorDBInt4Global._dequantize_int4   VectorDBInt4Global.py:166-188
+ *   VectorDBInt8._dequantize_int8         VectorDBInt8.py:129-138
+ *   VectorDBInt4._dequantize_int4         VectorDBInt4.py:157-184
+ * bit-identical to the reference (NumPy 2 scalar rules).  q is the code array (int8 / int16 /
+ * packed int4 bytes), minmax f64[n, 2] for the local modes (NULL otherwise), limit for the global
+ * ones.  vrq_dequantize writes f32[n, dim]; vrq_rescore_dequant writes, per (query, candidate), the
+ * reference score float(np.dot(query_float, dequantised row)) (VectorDBInt8Global.py:232-238 and the
+ * same loop in the other classes) as the correctly rounded float32 dot (NaN for negative rows).
+ * ------------------------------------------------------------------------- */
+int vrq_dequantize(int32_t mode, const void* q, const double* minmax, int64_t n, int32_t dim, double limit,
+                   float* out, void* stream);
+int vrq_rescore_dequant(int32_t mode, const float* qf, int32_t nq, int32_t dim, const void* q,
+                        const double* minmax, double limit, int64_t n, const int64_t* cand_rows,
+                        int32_t ncand, double* out, void* stream);
 /* np.linalg.norm(int8 row) in float64 (CohereEnhancedVectorDB.py:308), computed once at add time */
 int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, void* stream);
 /* ---------------------------------------------------------------------------

@@ -244,6 +244,43 @@ def exhaustive_topk(scores: np.ndarray, k: int):
     return np.array(out, dtype=np.int64)
 
 
+def dequantize(mode: str, q: np.ndarray, minmax: np.ndarray = None, limit: float = None, dim: int = 1024):
+    """Restatement of the VectorDB* ``_dequantize_*`` methods for a batch of rows (f32[n, dim]):
+    ``int8g`` VectorDBInt8Global.py:144-152, ``int16g`` VectorDBInt16Global.py:144-152, ``int4g``
+    VectorDBInt4Global.py:166-188, ``int8`` VectorDBInt8.py:129-138, ``int4`` VectorDBInt4.py:157-184."""
+    q = np.asarray(q)
+    if mode == "int8g":
+        return q.astype(np.float32) * np.float32(limit / 127.0)
+    if mode == "int16g":
+        return q.astype(np.float32) * np.float32(limit / 32767.0)
+    if mode in ("int4g", "int4"):
+        b = q.view(np.uint8).astype(np.int64)
+        nib = np.stack([(b >> 4) & 15, b & 15], axis=-1).reshape(q.shape[0], -1)[:, :dim]
+        if mode == "int4g":
+            return ((nib - 8) * (limit / 7.0)).astype(np.float32)
+        out = np.zeros((q.shape[0], dim), np.float32)
+        for r in range(q.shape[0]):
+            mn, mx = float(minmax[r, 0]), float(minmax[r, 1])
+            if mn != mx:
+                out[r] = ((nib[r] - 8) * (max(abs(mn), abs(mx)) / 7.0)).astype(np.float32)
+        return out
+    out = np.zeros(q.shape, np.float32)                      # "int8": np.float32 min / max
+    for r in range(q.shape[0]):
+        mn, mx = np.float32(minmax[r, 0]), np.float32(minmax[r, 1])
+        if mn != mx:
+            scale = np.float32(max(abs(mn), abs(mx)) / np.float32(127))
+            out[r] = q[r].astype(np.float32) * scale
+    return out
+
+
+def dequant_scores(qf: np.ndarray, deq: np.ndarray) -> np.ndarray:
+    """``float(np.dot(query_float, doc_emb))`` (VectorDBInt8Global.py:235) for every (query, row),
+    f64 [nq, n]: the float32 dot taken as the correctly rounded exact dot (the GPU's definition;
+    NumPy's sdot is within a few ulps of it)."""
+    return (np.asarray(qf, np.float32).astype(np.float64) @ np.asarray(deq, np.float32).astype(np.float64).T
+            ).astype(np.float32).astype(np.float64)
+
+
 def int8_row_norms(x: np.ndarray) -> np.ndarray:
     """``np.linalg.norm(doc_int8)`` per row (float64), ``CohereEnhancedVectorDB.py:308``."""
     x = np.asarray(x)

@@ -16,6 +16,8 @@ absent native dependencies stubbed:
 The reference's methods then run UNMODIFIED:
 * the static encoders ``_quantize_to_*`` / ``_to_binary`` of all six
   ``VectorDBInt{4,8,16}{,Global}`` classes  -> ``encoders.npz``;
+* their ``_dequantize_*`` methods on those codes and the search loop's rescoring expression
+  ``float(np.dot(query_float, doc_emb))``  -> ``dequant.npz``;
 * ``CohereEnhancedVectorDB.search`` (Phases I-III, ``:227-322``) and
   ``add_documents``/``remove_document`` (``:171-225,324-340``) with the HTTP
   embedding call replaced by a table lookup -> ``search_synth.npz``;
@@ -30,7 +32,7 @@ Safe loading: index.bin / index.faiss are raw FAISS binary formats read with
 nothing) is used to pull out the ``"doc"`` string and the raw 1024-byte int8
 payload.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real ...]
 """
 from __future__ import annotations
 
@@ -138,6 +140,41 @@ def gen_encoders(out_path: str):
             assert np.array_equal(O.to_binary(x), ref)
     np.savez_compressed(out_path, **res)
     print("wrote", out_path, sorted(res)[:6], "...")
+
+
+def gen_dequant(enc_path: str, out_path: str):
+    """The reference's own ``_dequantize_*`` methods on the encoder fixtures, and its rescoring
+    expression ``float(np.dot(query_float, doc_emb))`` (VectorDBInt8Global.py:235) for a few queries."""
+    E = np.load(enc_path)
+    I8G = _import_ref("VectorDBInt8Global").VectorDBInt8Global
+    I16G = _import_ref("VectorDBInt16Global").VectorDBInt16Global
+    I4G = _import_ref("VectorDBInt4Global").VectorDBInt4Global
+    I8 = _import_ref("VectorDBInt8").VectorDBInt8
+    I4 = _import_ref("VectorDBInt4").VectorDBInt4
+    rng = np.random.default_rng(99)
+    res = {}
+    d = 1024
+    qf = rng.standard_normal((4, d)).astype(np.float32) * 0.03
+    res["qf"] = qf
+    for tag in ("l03", "l01", "l10"):
+        lim = float(E[f"limit_{tag}"])
+        res[f"int8g_{tag}"] = np.stack([I8G._dequantize_int8(x, lim) for x in E[f"int8g_{tag}_{d}"]])
+        res[f"int16g_{tag}"] = np.stack([I16G._dequantize_int16(x, lim) for x in E[f"int16g_{tag}_{d}"]])
+        # int4: the packed bytes go in as Python ints.  Under NumPy >= 2 the reference's nibble loop
+        # (`byte + 256` on np.int8, `nibble - 8` on np.uint8) raises OverflowError / wraps around;
+        # with Python ints the unmodified code computes what it computed under NumPy 1.
+        res[f"int4g_{tag}"] = np.stack([I4G._dequantize_int4([int(b) for b in x], d, lim)
+                                        for x in E[f"int4g_{tag}_{d}"]])
+    mm8 = E[f"int8_minmax_{d}"]
+    res["int8"] = np.stack([I8._dequantize_int8(x, (np.float32(a), np.float32(b)))
+                            for x, (a, b) in zip(E[f"int8_{d}"], mm8)])
+    mm4 = E[f"int4_minmax_{d}"]
+    res["int4"] = np.stack([I4._dequantize_int4([int(v) for v in x], d, (float(a), float(b)))
+                            for x, (a, b) in zip(E[f"int4_{d}"], mm4)])
+    for key in [k for k in res if k != "qf"]:
+        res[f"score_{key}"] = np.array([[float(np.dot(q, row)) for row in res[key]] for q in qf])
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
 
 
 # ---------------------------------------------------------------------------
@@ -381,6 +418,12 @@ def gen_search_real(out_path: str):
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference checkout not mounted; fixtures are generated in the build container only")
-    gen_encoders(os.path.join(HERE, "encoders.npz"))
-    gen_search_synth(os.path.join(HERE, "search_synth.npz"))
-    gen_search_real(os.path.join(HERE, "search_real.npz"))
+    only = sys.argv[1:]  # e.g. "dequant": regenerate just that fixture
+    if not only or "encoders" in only:
+        gen_encoders(os.path.join(HERE, "encoders.npz"))
+    if not only or "dequant" in only:
+        gen_dequant(os.path.join(HERE, "encoders.npz"), os.path.join(HERE, "dequant.npz"))
+    if not only or "search_synth" in only:
+        gen_search_synth(os.path.join(HERE, "search_synth.npz"))
+    if not only or "search_real" in only:
+        gen_search_real(os.path.join(HERE, "search_real.npz"))

@@ -127,3 +127,34 @@ def test_binary_flat_search_against_brute_force_definition():
         order = sorted(range(500), key=lambda r: (dist[r], r))[:20]
         assert I[j].tolist() == order
         assert D[j].tolist() == [int(dist[r]) for r in order]
+
+
+DEQ_KEYS = ["int8g_l03", "int8g_l01", "int8g_l10", "int16g_l03", "int16g_l01", "int16g_l10",
+            "int4g_l03", "int4g_l01", "int4g_l10", "int8", "int4"]
+
+
+def deq_inputs(E, key):
+    """(mode, codes, minmax, limit) of a dequant fixture key, from the encoder fixture it was built on."""
+    mode, _, tag = key.partition("_")
+    if mode in ("int8", "int4"):
+        return mode, E[f"{mode}_1024"], E[f"{mode}_minmax_1024"], 0.0
+    return mode, E[f"{mode}_{tag}_1024"], None, float(E[f"limit_{tag}"])
+
+
+def score_close(got, ref, q, deq):
+    """float32-dot parity: 1e-5 relative, with the float32 summation floor near zero."""
+    scale = np.abs(q.astype(np.float64) * deq.astype(np.float64)).sum()
+    return np.abs(got - ref) <= 1e-5 * np.maximum(np.abs(ref), 1e-2 * scale)
+
+
+@pytest.mark.parametrize("key", DEQ_KEYS)
+def test_dequantize_oracle_matches_reference(golden, key):
+    """VectorDB*._dequantize_* (the reference's own methods, golden) == the oracle restatement, bit for bit;
+    the rescoring expression float(np.dot(q, row)) within the float32-dot tolerance."""
+    E, G = golden["encoders"], golden["dequant"]
+    mode, q, mm, lim = deq_inputs(E, key)
+    D = O.dequantize(mode, q, mm, lim)
+    assert np.array_equal(D, G[key])
+    S = O.dequant_scores(G["qf"], D)
+    for qi in range(G["qf"].shape[0]):
+        assert np.all(score_close(S[qi], G[f"score_{key}"][qi], G["qf"][qi], D))

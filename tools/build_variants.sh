@@ -15,7 +15,7 @@ wait
 for spec in "$@"; do
   name=${spec%%=*}; rest=${spec#*=}; src=${rest%%:*}
   objs=""
-  for s in hamming_scan hamming_mfma select_rescore encode gemm_topk; do
+  for s in hamming_scan hamming_mfma select_rescore encode gemm_topk dequant; do
     if [ "$s.hip" = "$src" ]; then objs="$objs tools/probes/g5/${name}_$s.o"; else objs="$objs $OBJ/$s.o"; fi
   done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o tools/probes/g5/lib_$name.so

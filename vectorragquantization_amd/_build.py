@@ -16,7 +16,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvrq.so")
 OBJDIR = os.path.join(PKG, "_obj")
-SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode.hip", "gemm_topk.hip"]
+SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode.hip", "gemm_topk.hip", "dequant.hip"]
 ARCH = os.environ.get("VRQ_OFFLOAD_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]

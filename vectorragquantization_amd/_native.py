@@ -63,6 +63,8 @@ SIGNATURES = {
     "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),
     "vrq_encode": (C.c_int, [_I32, _P, _I64, _I32, _D, _P, _P, _P, _P]),
     "vrq_int8_row_norms": (C.c_int, [_P, _I64, _I32, _P, _P]),
+    "vrq_dequantize": (C.c_int, [_I32, _P, _P, _I64, _I32, _D, _P, _P]),
+    "vrq_rescore_dequant": (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _D, _I64, _P, _I32, _P, _P]),
     "vrq_gemm_topk_workspace_size": (_SZ, [_I32, _I64, _I32, _I32, _I32]),
     "vrq_gemm_topk_pieces": (C.c_int, []),
     "vrq_gemm_topk": (C.c_int, [_I32, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,

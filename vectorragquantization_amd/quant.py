@@ -59,6 +59,64 @@ def encode(mode: str, X, limit: float = 0.3, device=None) -> dict:
     return {"codes": codes, "q": q, "minmax": mm}
 
 
+_DEQ_MODES = {"int8g": 0, "int16g": 1, "int4g": 2, "int8": 3, "int4": 4}
+
+
+def dequantize(mode: str, q, minmax=None, limit: float = 0.0, dim: int = None, device=None) -> torch.Tensor:
+    """Device ``_dequantize_*`` of the VectorDB* classes for a batch of rows (``vrq_dequantize``):
+    ``int8g``/``int16g``/``int4g`` take the global ``limit``, ``int8``/``int4`` the per-row
+    (min, max) f64[n, 2].  Returns f32[n, dim] on the device, bit-identical to the reference."""
+    dev = _device(device)
+    dt = {"int8g": torch.int8, "int8": torch.int8, "int16g": torch.int16, "int4g": torch.int8, "int4": torch.int8}[mode]
+    q = as_device_tensor(q, dt, dev)
+    if q.dim() == 1:
+        q = q.reshape(1, -1)
+    n = q.shape[0]
+    d = dim if dim is not None else (2 * q.shape[1] if mode in ("int4g", "int4") else q.shape[1])
+    mm = as_device_tensor(np.asarray(minmax, np.float64).reshape(n, 2), torch.float64, dev) if minmax is not None else None
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    lib = N.load()
+    with torch.cuda.device(dev):
+        rc = lib.vrq_dequantize(_DEQ_MODES[mode], N.ptr(q), N.ptr(mm), n, d, float(limit), N.ptr(out),
+                                N.stream_handle(dev))
+    N.check(rc, f"vrq_dequantize({mode})")
+    return out
+
+
+def vectordb_search(mode: str, codes: torch.Tensor, q: torch.Tensor, qf: torch.Tensor, qb: torch.Tensor, k: int = 10,
+                    binary_oversample: int = 10, minmax: torch.Tensor = None, limit: float = 0.0):
+    """``VectorDBInt{4,8,16}{,Global}.search`` for a query batch (e.g. VectorDBInt8Global.py:205-243):
+    Phase I Hamming top-``k * binary_oversample`` over the ubinary codes (``vrq_hamming_topk``, FAISS
+    order), Phase II ``float(np.dot(query_float, dequantised row))`` (``vrq_rescore_dequant``), stable
+    sort by score descending, first k.  ``mode="bin16"`` (VectorDBInt16.search) stops after Phase I
+    and ranks by Hamming distance.  Returns (rows i64[nq, k], hamming i32[nq, k], score f64[nq, k])
+    on the device; rows past the corpus are -1 (score NaN)."""
+    dev = codes.device
+    n, cb = codes.shape
+    nq = qb.shape[0]
+    K = min(k * binary_oversample, n)
+    lib = N.load()
+    dist = torch.empty((nq, K), dtype=torch.int32, device=dev)
+    rows = torch.empty((nq, K), dtype=torch.int64, device=dev)
+    ws = torch.empty((max(8, lib.vrq_hamming_topk_workspace_size(n, cb, nq, K)),), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        N.check(lib.vrq_hamming_topk(N.ptr(codes), n, cb, 0, N.ptr(qb), nq, K, N.ptr(dist), N.ptr(rows), N.ptr(ws),
+                                     ws.numel(), N.stream_handle(dev)), "vrq_hamming_topk")
+    if mode == "bin16":
+        kk = min(k, K)
+        return rows[:, :kk], dist[:, :kk], dist[:, :kk].to(torch.float64)
+    score = torch.empty((nq, K), dtype=torch.float64, device=dev)
+    d = qf.shape[1]
+    with torch.cuda.device(dev):
+        N.check(lib.vrq_rescore_dequant(_DEQ_MODES[mode], N.ptr(qf), nq, d, N.ptr(q), N.ptr(minmax), float(limit), n,
+                                        N.ptr(rows), K, N.ptr(score), N.stream_handle(dev)), "vrq_rescore_dequant")
+    # Python's stable sort by score desc over the Phase-I order (VectorDBInt8Global.py:241);
+    # missing candidates (-1) sort last, -0.0 ties +0.0
+    key = torch.where(rows >= 0, score + 0.0, torch.full_like(score, float("-inf")))
+    o = torch.sort(-key, dim=1, stable=True).indices[:, :k]
+    return torch.gather(rows, 1, o), torch.gather(dist, 1, o), torch.gather(score, 1, o)
+
+
 def int8_row_norms(x8: torch.Tensor) -> torch.Tensor:
     """float64 ``np.linalg.norm`` of every int8 row (``CohereEnhancedVectorDB.py:308``)."""
     x8 = x8.contiguous()
@@ -96,8 +154,9 @@ class VectorDBInt8Global(_Binary):
 
     @staticmethod
     def _dequantize_int8(emb_int8, limit: float):
-        """``VectorDBInt8Global.py:144-152``: int8 * float32(limit/127)."""
-        return np.asarray(emb_int8).astype(np.float32) * (limit / 127.0)
+        """``VectorDBInt8Global.py:144-152``: int8 * float32(limit/127) (on the device)."""
+        one = np.ndim(emb_int8) == 1
+        return _host(dequantize("int8g", emb_int8, limit=limit), one)
 
 
 class VectorDBInt16Global(_Binary):
@@ -108,8 +167,9 @@ class VectorDBInt16Global(_Binary):
 
     @staticmethod
     def _dequantize_int16(emb_int16, limit: float):
-        """``VectorDBInt16Global.py:144-152``."""
-        return np.asarray(emb_int16).astype(np.float32) * (limit / 32767.0)
+        """``VectorDBInt16Global.py:144-152`` (on the device)."""
+        one = np.ndim(emb_int16) == 1
+        return _host(dequantize("int16g", emb_int16, limit=limit), one)
 
 
 class VectorDBInt4Global(_Binary):
@@ -118,6 +178,12 @@ class VectorDBInt4Global(_Binary):
         """Reproduces the reference: ``limit`` is ignored (per-vector 7/max|x| scale)."""
         one = np.ndim(embedding) == 1
         return _host(encode("int4g", embedding, 1.0)["q"], one)
+
+    @staticmethod
+    def _dequantize_int4(q_packed, length: int, limit: float):
+        """``VectorDBInt4Global.py:166-188`` (on the device)."""
+        one = np.ndim(q_packed) == 1
+        return _host(dequantize("int4g", np.asarray(q_packed).astype(np.int8), limit=limit, dim=length), one)
 
 
 class VectorDBInt8(_Binary):
@@ -130,6 +196,12 @@ class VectorDBInt8(_Binary):
             return q, np.float32(mm[0, 0]), np.float32(mm[0, 1])
         return q, mm.astype(np.float32)[:, 0], mm.astype(np.float32)[:, 1]
 
+    @staticmethod
+    def _dequantize_int8(emb_int8, min_max):
+        """``VectorDBInt8.py:129-138`` (on the device); min_max = (min, max) or an [n, 2] array."""
+        one = np.ndim(emb_int8) == 1
+        return _host(dequantize("int8", emb_int8, minmax=np.asarray(min_max, np.float64)), one)
+
 
 class VectorDBInt4(_Binary):
     @staticmethod
@@ -140,6 +212,13 @@ class VectorDBInt4(_Binary):
         if one:
             return q, float(mm[0, 0]), float(mm[0, 1])
         return q, mm[:, 0], mm[:, 1]
+
+    @staticmethod
+    def _dequantize_int4(q_packed, length: int, min_max):
+        """``VectorDBInt4.py:157-184`` (on the device)."""
+        one = np.ndim(q_packed) == 1
+        return _host(dequantize("int4", np.asarray(q_packed).astype(np.int8), minmax=np.asarray(min_max, np.float64),
+                                dim=length), one)
 
 
 class VectorDBInt16:
