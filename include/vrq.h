@@ -230,6 +230,29 @@ int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const do
                   int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
                   int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,
                   size_t workspace_bytes, void* stream);
+/* ---------------------------------------------------------------------------
+ * Exact float inner-product top-k: CohereVectorDBFloat's faiss.IndexIDMap(faiss.IndexFlatIP(d))
+ * (CohereVectorDBFloat.py:55-64) searched at :156, for a batch of queries, on the matrix cores.
+ *   s = q . x in float32 (the exact products summed in float64, rounded once to float32)
+ * out_* as vrq_gemm_topk: the k rows with the largest s ordered (s desc, row asc) -- FAISS's
+ * IndexFlatIP result order, re-sorted stably by score at :170 -- as row_offset + row, scores f64
+ * holding the float32 values.
+ * vrq_flat_ip_prepare (once per added batch, rows [0, n) of the given pointers) derives the
+ * matrix pass's operands from the float32 rows xf: x8 int8[n, dim] (per-row scaled), inv_scale
+ * f64[n] and the running corpus bounds f64[2], which it max-accumulates (zero them before the first
+ * batch; after removals the old bounds stay valid upper bounds).  vrq_flat_ip_topk: exact for every
+ * input -- int8 queries x int8 rows on v_mfma_i32_32x32x32_i8 within a proven per-query bound, a
+ * sampled threshold, exact rescoring of the survivors from xf (exact fallback on heavy ties).
+ * Workspace: vrq_gemm_topk_workspace_size(VRQ_GEMM_FLOAT_IP, ...).  Supported: dim = 1024,
+ * 1 <= k <= 1024, 1 <= n < 2^32, finite inputs.
+ * ------------------------------------------------------------------------- */
+#define VRQ_GEMM_FLOAT_IP 4
+int vrq_flat_ip_prepare(const float* xf, int64_t n, int32_t dim, int8_t* x8, double* inv_scale, double* bounds,
+                        void* stream);
+int vrq_flat_ip_topk(const float* xf, const int8_t* x8, const double* inv_scale, const double* bounds, int64_t n,
+                     int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
+                     int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -298,6 +298,69 @@ def float_ip_topk(F: np.ndarray, Q: np.ndarray, k: int) -> np.ndarray:
     return out
 
 
+def flat_ip_scores(F: np.ndarray, Q: np.ndarray) -> np.ndarray:
+    """IndexFlatIP scores q . x (``CohereVectorDBFloat.py:62,156``) for every (query, row), f64
+    [nq, n] holding float32 values: the exact f64 dot rounded once to float32 (the GPU's
+    definition; FAISS's sgemm rounds per step and lands within the float32 summation error)."""
+    return (np.asarray(Q, np.float32).astype(np.float64) @ np.asarray(F, np.float32).astype(np.float64).T
+            ).astype(np.float32).astype(np.float64)
+
+
+def flat_ip_search(F: np.ndarray, Q: np.ndarray, k: int, chunk: int = 64):
+    """FAISS ``IndexFlatIP.search`` restated: per query the k largest ``flat_ip_scores`` ordered
+    (score desc, row asc) -- FAISS's result order for IP; the reference then re-sorts stably by
+    score (``CohereVectorDBFloat.py:170``), which keeps it.  Returns (scores f64[nq, k'], rows
+    i64[nq, k']) with k' = min(k, n)."""
+    F = np.asarray(F, np.float32)
+    Q = np.asarray(Q, np.float32).reshape(-1, F.shape[1])
+    kk = min(k, F.shape[0])
+    rows = np.empty((Q.shape[0], kk), np.int64)
+    sc = np.empty((Q.shape[0], kk), np.float64)
+    idx = np.arange(F.shape[0])
+    for c in range(0, Q.shape[0], chunk):
+        S = flat_ip_scores(F, Q[c:c + chunk])
+        for j in range(S.shape[0]):
+            o = np.lexsort((idx, -S[j]))[:kk]
+            rows[c + j] = o
+            sc[c + j] = S[j, o]
+    return sc, rows
+
+
+class IndexFlatIPIDMap:
+    """NumPy restatement of ``faiss.IndexIDMap(faiss.IndexFlatIP(d))`` as the reference drives it
+    (``CohereVectorDBFloat.py:62`` build, ``:133`` add_with_ids, ``:156`` search, ``:177``
+    remove_ids): rows in insertion order, ``remove_ids`` compacts keeping the survivors' order,
+    labels are ``id_map[row]``, -1 past ntotal."""
+
+    def __init__(self, d: int = 1024):
+        self.d = d
+        self.xb = np.zeros((0, d), np.float32)
+        self.id_map = np.zeros((0,), np.int64)
+
+    @property
+    def ntotal(self) -> int:
+        return int(self.xb.shape[0])
+
+    def add_with_ids(self, x, ids) -> None:
+        self.xb = np.concatenate([self.xb, np.asarray(x, np.float32).reshape(-1, self.d)])
+        self.id_map = np.concatenate([self.id_map, np.asarray(ids, np.int64).reshape(-1)])
+
+    def search(self, q, k: int):
+        q = np.asarray(q, np.float32).reshape(-1, self.d)
+        D = np.full((q.shape[0], k), -np.finfo(np.float32).max, np.float32)
+        L = np.full((q.shape[0], k), -1, np.int64)
+        if self.ntotal:
+            sc, rows = flat_ip_search(self.xb, q, k)
+            D[:, :rows.shape[1]] = sc.astype(np.float32)
+            L[:, :rows.shape[1]] = self.id_map[rows]
+        return D, L
+
+    def remove_ids(self, ids) -> int:
+        keep = ~np.isin(self.id_map, np.asarray(ids, np.int64))
+        self.xb, self.id_map = self.xb[keep], self.id_map[keep]
+        return int((~keep).sum())
+
+
 # --------------------------------------------------------------------------
 # Encoders (VectorDBInt{4,8,16}{,Global}); literal restatements
 # --------------------------------------------------------------------------

@@ -17,7 +17,7 @@ def pytest_configure(config):
 def golden():
     import numpy as np
     return {name: np.load(os.path.join(GOLDEN, f"{name}.npz"))
-            for name in ("encoders", "search_synth", "search_real", "dequant")}
+            for name in ("encoders", "search_synth", "search_real", "dequant", "flat_real")}
 
 
 @pytest.fixture(scope="session")

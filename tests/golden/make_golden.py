@@ -32,7 +32,11 @@ Safe loading: index.bin / index.faiss are raw FAISS binary formats read with
 nothing) is used to pull out the ``"doc"`` string and the raw 1024-byte int8
 payload.
 
-Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real ...]
+* ``CohereVectorDBFloat.add_documents/remove_document/search`` (``:103-180``) on the
+  reference's persisted float data (faiss's IndexIDMap(IndexFlatIP) = the oracle
+  restatement) -> ``flat_real.npz``.
+
+Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real|flat_real ...]
 """
 from __future__ import annotations
 
@@ -65,6 +69,15 @@ def _install_stubs():
     faiss.IndexBinaryIDMap2 = lambda flat: O.IndexBinaryIDMap2(flat.d)
     faiss.write_index_binary = lambda index, path: None
     faiss.read_index_binary = lambda path: (_ for _ in ()).throw(RuntimeError("no faiss"))
+
+    class _FlatIP:  # IndexFlatIP(d) placeholder: carries d only
+        def __init__(self, d):
+            self.d = d
+
+    faiss.IndexFlatIP = _FlatIP
+    faiss.IndexIDMap = lambda flat: O.IndexFlatIPIDMap(flat.d)
+    faiss.write_index = lambda index, path: None
+    faiss.read_index = lambda path: (_ for _ in ()).throw(RuntimeError("no faiss"))
     sys.modules["faiss"] = faiss
     rd = types.ModuleType("rocksdict")
     rd.Rdict = dict
@@ -415,6 +428,49 @@ def gen_search_real(out_path: str):
     print("wrote", out_path, "recall@10 vs float32 =", rec)
 
 
+def gen_flat_real(out_path: str):
+    """``CohereVectorDBFloat`` (``CohereVectorDBFloat.py:103-172``) run unmodified on the reference's
+    persisted 1000-document float data (``db_cohere_float/index.faiss``): add_documents of all 1000
+    in 64-doc batches, remove_document of two ids and re-add of one (compaction + order), then
+    search for 100 document-vector queries and 60 perturbed ones at k = 10 and k = 50."""
+    path = os.path.join(REF, "db_cohere_float/index.faiss")
+    F, fid = read_ixmp_flat(path)
+    assert np.array_equal(fid, np.arange(1000))
+    CF = _import_ref("CohereVectorDBFloat").CohereVectorDBFloat
+    db = object.__new__(CF)            # skip __init__ (env vars / folders)
+    db.folder = "/nonexistent"
+    db.index = __import__("faiss").IndexIDMap(__import__("faiss").IndexFlatIP(1024))
+    db.doc_db = {}
+    lookup = {f"d{i}": F[i] for i in range(1000)}
+    db._generate_float_embeddings = lambda texts, input_type: {t: lookup[t] for t in texts}
+    db.save = lambda: None
+    db.add_documents(list(range(1000)), [f"d{i}" for i in range(1000)], batch_size=64, save=False)
+    db.remove_document(5, save=False)
+    db.remove_document(17, save=False)
+    db.add_documents([5], ["d5"], save=False)   # re-added: now the last row
+    rng = np.random.default_rng(11)
+    qsrc = np.arange(0, 1000, 10)
+    P = F[rng.integers(0, 1000, 60)] + 0.3 * rng.standard_normal((60, 1024)).astype(np.float32) / 32.0
+    QF = np.concatenate([F[qsrc], P / np.linalg.norm(P, axis=1, keepdims=True)]).astype(np.float32)
+    res = {"xf": F, "qf": QF, "row_ids": db.index.id_map.copy(),
+           "index_faiss_sha256": np.frombuffer(__import__("hashlib").sha256(open(path, "rb").read()).digest(),
+                                               np.uint8)}
+    for k in (10, 50):
+        ids = np.full((QF.shape[0], k), -1, np.int64)
+        sc = np.full((QF.shape[0], k), np.nan)
+        cnt = np.zeros(QF.shape[0], np.int64)
+        for j in range(QF.shape[0]):
+            lookup[f"q{j}"] = QF[j]
+            r = db.search(f"q{j}", k=k)
+            cnt[j] = len(r)
+            for i, h in enumerate(r):
+                ids[j, i] = h["doc_id"]
+                sc[j, i] = h["score"]
+        res.update({f"k{k}_ids": ids, f"k{k}_score": sc, f"k{k}_cnt": cnt})
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference checkout not mounted; fixtures are generated in the build container only")
@@ -427,3 +483,5 @@ if __name__ == "__main__":
         gen_search_synth(os.path.join(HERE, "search_synth.npz"))
     if not only or "search_real" in only:
         gen_search_real(os.path.join(HERE, "search_real.npz"))
+    if not only or "flat_real" in only:
+        gen_flat_real(os.path.join(HERE, "flat_real.npz"))

@@ -48,3 +48,19 @@ def test_http_provider_requires_env_like_reference(monkeypatch):
     assert p.endpoint.endswith("/v2/embed")
     # no network: failures are logged and {} returned, as in CohereEnhancedVectorDB.py:167-169
     assert p.embed(["x"], "search_query", ["float"]) == {}
+
+
+def test_ixmp_pack_reproduces_reference_index_faiss(golden):
+    """FloatIndexIDMap's writer: the reference's db_cohere_float/index.faiss byte-for-byte (its
+    sha256 is in the fixture), and the reader inverts it."""
+    from vectorragquantization_amd.flat import ixmp_pack, ixmp_unpack
+    g = golden["flat_real"]
+    b = ixmp_pack(1024, g["xf"], np.arange(1000))
+    assert hashlib.sha256(b).digest() == g["index_faiss_sha256"].tobytes()
+    d, xf, ids = ixmp_unpack(b)
+    assert d == 1024 and np.array_equal(xf, g["xf"]) and np.array_equal(ids, np.arange(1000))
+    with pytest.raises(ValueError):
+        ixmp_unpack(b"IBM2" + b[4:])
+    e = ixmp_pack(1024, np.zeros((0, 1024), np.float32), np.zeros(0, np.int64))
+    d, xf, ids = ixmp_unpack(e)
+    assert xf.shape == (0, 1024) and ids.shape == (0,)

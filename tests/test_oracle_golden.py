@@ -158,3 +158,42 @@ def test_dequantize_oracle_matches_reference(golden, key):
     S = O.dequant_scores(G["qf"], D)
     for qi in range(G["qf"].shape[0]):
         assert np.all(score_close(S[qi], G[f"score_{key}"][qi], G["qf"][qi], D))
+
+
+@pytest.mark.parametrize("k", [10, 50])
+def test_flat_ip_oracle_matches_reference_real_data(golden, k):
+    """IndexFlatIP restatement driven by the reference's own CohereVectorDBFloat (add in batches,
+    remove, re-add, search, stable re-sort) on its persisted float data: identical labels and
+    scores; and the restated scores agree with a plain float32 BLAS product (FAISS's sgemm path)
+    within the float32 summation error."""
+    g = golden["flat_real"]
+    idx = O.IndexFlatIPIDMap(1024)
+    for s in range(0, 1000, 64):
+        idx.add_with_ids(g["xf"][s:s + 64], np.arange(s, min(s + 64, 1000)))
+    idx.remove_ids([5])
+    idx.remove_ids([17])
+    idx.add_with_ids(g["xf"][5:6], [5])
+    assert np.array_equal(idx.id_map, g["row_ids"])
+    D, L = idx.search(g["qf"], k)
+    assert np.array_equal(L, g[f"k{k}_ids"])
+    assert np.array_equal(D.astype(np.float64), g[f"k{k}_score"])
+    S32 = (g["qf"] @ idx.xb.T).astype(np.float64)
+    bound = 1e-6 * (np.abs(g["qf"]) @ np.abs(idx.xb).T)
+    S = O.flat_ip_scores(idx.xb, g["qf"])
+    assert np.all(np.abs(S - S32) <= bound)
+
+
+def test_flat_ip_search_definition_small():
+    """flat_ip_search on a tiny case by brute force: ties by lower row, k > n truncated."""
+    rng = np.random.default_rng(3)
+    F = rng.standard_normal((9, 1024)).astype(np.float32)
+    F[4] = F[1]
+    F[7] = 0.0
+    Q = np.stack([F[1], np.zeros(1024, np.float32), -F[2]])
+    sc, rows = O.flat_ip_search(F, Q, 20)
+    assert rows.shape == (3, 9)
+    assert rows[0][:2].tolist() == [1, 4]
+    assert rows[1].tolist() == list(range(9))
+    for q in range(3):
+        exact = [float(np.float32(np.dot(Q[q].astype(np.float64), F[r].astype(np.float64)))) for r in rows[q]]
+        assert sc[q].tolist() == exact

@@ -28,6 +28,7 @@ VRQ_SCAN_STAGE_SUFFIX = 64
 VRQ_SCAN_STAGE_RECHECK = 128
 VRQ_GEMM_BINARY = 2
 VRQ_GEMM_INT8_COSINE = 3
+VRQ_GEMM_FLOAT_IP = 4
 VRQ_GEMM_STAGE_SAMPLE = 16
 VRQ_GEMM_STAGE_MAIN = 32
 VRQ_GEMM_STAGE_FINISH = 64
@@ -69,6 +70,9 @@ SIGNATURES = {
     "vrq_gemm_topk_pieces": (C.c_int, []),
     "vrq_gemm_topk": (C.c_int, [_I32, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,
                                 _P]),
+    "vrq_flat_ip_prepare": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),
+    "vrq_flat_ip_topk": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,
+                                   _P]),
 }
 
 

@@ -42,6 +42,23 @@ __device__ __forceinline__ double phase3_cos(const float (&qv)[DPL], const int8_
   return nrm == 0.0 ? -__builtin_inf() : (double)f / nrm;
 }
 
+// IndexFlatIP (CohereVectorDBFloat.py:62,156): the float32 inner product q . x, computed as the
+// exact products summed in float64 and rounded once to float32 (FAISS's sgemm / fvec_inner_product
+// round at every step; this is the same value within the float32 summation error).
+__device__ __forceinline__ double flat_ip(const float (&qv)[DPL], const float* __restrict__ xrow) {
+  const float4* p = reinterpret_cast<const float4*>(xrow + DPL * lane_id());
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < DPL / 4; ++i) {
+    const float4 v = p[i];
+    s += (double)qv[4 * i + 0] * (double)v.x;
+    s += (double)qv[4 * i + 1] * (double)v.y;
+    s += (double)qv[4 * i + 2] * (double)v.z;
+    s += (double)qv[4 * i + 3] * (double)v.w;
+  }
+  return (double)(float)wave_sum_f64(s);
+}
+
 __device__ __forceinline__ void load_q(float (&qv)[DPL], const float* __restrict__ q) {
   const int l = lane_id();
   const float4* p = reinterpret_cast<const float4*>(q + DPL * l);

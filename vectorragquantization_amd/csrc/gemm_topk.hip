@@ -135,7 +135,8 @@ __device__ __forceinline__ int xcd_logical(int b, int nb) {
 // prep: one wave per (padded) query.  qa[q] = pieces a, b in fragment order (natural k order for
 // Phase III, ph2_pos for Phase II); delta[q] = Delta_q in u units.
 __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* __restrict__ qf, int nq, int nq_pad,
-                                                        int8_t* __restrict__ qa, double* __restrict__ delta) {
+                                                        int8_t* __restrict__ qa, double* __restrict__ delta,
+                                                        const double* __restrict__ bounds) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
   if (q >= nq_pad) return;
   int8_t* o = qa + (int64_t)q * QA_BYTES;
@@ -186,8 +187,18 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   q1 = wave_sum_f64(q1);
   constexpr double SLACK = 1.0 / (1 << 20);  // >= 16 f32 ulps of every rounding on the u path
   if (l == 0) {
-    const double d = mode == VRQ_GEMM_BINARY ? r1 * (1.0 + SLACK) + SLACK * q1 * invS
-                                             : sqrt(r2) * (1.0 + SLACK) + SLACK * sqrt(q2) * invS;
+    double d;
+    if (mode == VRQ_GEMM_BINARY) {
+      d = r1 * (1.0 + SLACK) + SLACK * q1 * invS;
+    } else if (mode == VRQ_GEMM_FLOAT_IP) {
+      // u = s_r <a, b_r> against s' = <q/S, x_r> with x_r = s_r b_r + sigma_r (flat_ip_prepare):
+      // |u - s'| <= ||rho|| ||s_r b_r|| + ||q/S|| ||sigma_r|| <= ||rho|| Bx + ||q/S|| Bsigma, and
+      // |u| <= ||a|| Bx <= (||q/S|| + ||rho||) Bx scales the f32 slack
+      const double qn = sqrt(q2) * invS, rn = sqrt(r2), bx = bounds[0], bs = bounds[1];
+      d = (rn * bx + qn * bs) * (1.0 + SLACK) + SLACK * (qn + rn) * bx;
+    } else {
+      d = sqrt(r2) * (1.0 + SLACK) + SLACK * sqrt(q2) * invS;
+    }
     delta[q] = d;
   }
 }
@@ -633,13 +644,22 @@ __device__ inline void block_sort_pairs(uint64_t* key, uint32_t* row, int n_pow2
   __syncthreads();
 }
 
+// the corpus arrays a score reads (unused ones NULL)
+struct Rows {
+  const uint8_t* codes;  // VRQ_GEMM_BINARY: packed ubinary rows
+  const int8_t* x8;      // VRQ_GEMM_INT8_COSINE: int8 rows
+  const double* norms;   //   ... and their ||int8||_2
+  const float* xf;       // VRQ_GEMM_FLOAT_IP: float32 rows
+};
+
 template <int PH>
-__device__ __forceinline__ double exact_score(const float (&qv)[DPL], const uint8_t* codes, const int8_t* x8,
-                                              const double* norms, int64_t row) {
+__device__ __forceinline__ double exact_score(const float (&qv)[DPL], const Rows& c, int64_t row) {
   if constexpr (PH == VRQ_GEMM_BINARY)
-    return phase2_dot(qv, codes + row * (DIM / 8));
+    return phase2_dot(qv, c.codes + row * (DIM / 8));
+  else if constexpr (PH == VRQ_GEMM_FLOAT_IP)
+    return flat_ip(qv, c.xf + row * DIM);
   else
-    return phase3_cos(qv, x8 + row * DIM, norms[row]);
+    return phase3_cos(qv, c.x8 + row * DIM, c.norms[row]);
 }
 
 // Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
@@ -647,9 +667,8 @@ __device__ __forceinline__ double exact_score(const float (&qv)[DPL], const uint
 // (score desc, row asc), so the sort runs rarely once the list is full.  key/row[0..kc) hold the
 // running list in order.  All threads of the block call it; returns kc = min(k, count).
 template <int PH, class RowAt>
-__device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const uint8_t* codes,
-                            const int8_t* x8, const double* norms, int k, uint64_t* key, uint32_t* row,
-                            int32_t* fill) {
+__device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const Rows& c, int k,
+                            uint64_t* key, uint32_t* row, int32_t* fill) {
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
   if (tid == 0) *fill = 0;
   int kc = 0;
@@ -660,7 +679,7 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
     const int64_t end = base + FB_BATCH < count ? base + FB_BATCH : count;
     for (int64_t j = base + w; j < end; j += 4) {
       const uint32_t rr = row_at(j);
-      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, codes, x8, norms, (int64_t)rr));
+      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, c, (int64_t)rr));
       const bool take = kc < k || key_r < kk || (key_r == kk && rr < kr);
       if (take && l == 0) {
         const int i = kc + atomicAdd(fill, 1);
@@ -698,9 +717,7 @@ struct FinShared {
 // overflow (rows the main pass could not record) or fewer than min(k, n) candidates (zero-norm rows)
 // flags the query for the fallback instead.
 template <int PH>
-__global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restrict__ codes,
-                                                          const int8_t* __restrict__ x8,
-                                                          const double* __restrict__ norms, int64_t n,
+__global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t n,
                                                           int64_t row_offset, const float* __restrict__ qf, int k,
                                                           const uint32_t* __restrict__ cand,
                                                           const int32_t* __restrict__ ccnt, int nchunks, int capc,
@@ -749,7 +766,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restr
   };
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  const int kc = running_topk<PH>(total, row_at, qv, codes, x8, norms, k, sh.key, sh.row, &sh.misc[2]);
+  const int kc = running_topk<PH>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2]);
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)sh.row[i] + row_offset : -1;
@@ -764,9 +781,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const uint8_t* __restr
 // fallback: exact running top-k over every row for the flagged queries (list overflow from heavy
 // ties, zero-norm rows).  One workgroup per flagged query.
 template <int PH>
-__global__ __launch_bounds__(256) void gemm_fallback_kernel(const uint8_t* __restrict__ codes,
-                                                            const int8_t* __restrict__ x8,
-                                                            const double* __restrict__ norms, int64_t n,
+__global__ __launch_bounds__(256) void gemm_fallback_kernel(const Rows c, int64_t n,
                                                             int64_t row_offset, const float* __restrict__ qf, int k,
                                                             int32_t* __restrict__ out_count,
                                                             int64_t* __restrict__ out_rows,
@@ -780,7 +795,7 @@ __global__ __launch_bounds__(256) void gemm_fallback_kernel(const uint8_t* __res
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
   const int kc =
-      running_topk<PH>(n, [](int64_t j) { return (uint32_t)j; }, qv, codes, x8, norms, k, key, row, &fill);
+      running_topk<PH>(n, [](int64_t j) { return (uint32_t)j; }, qv, c, k, key, row, &fill);
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)row[i] + row_offset : -1;
@@ -845,6 +860,62 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   return VRQ_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// IndexFlatIP corpus preparation (vrq_flat_ip_prepare): one wave per float32 row x_r.
+//   s_r = max|x_r| / 127, b_r = clamp(rint(x_r / s_r), +-127) -> x8 (the matrix pass's int8 rows),
+//   inv_scale[r] = 1 / s_r (the pass multiplies the exact i32 dot by fl32(1 / fl32(inv_scale)) =
+//   s_r within 2^-22, inside the prep kernel's slack), and the running corpus bounds
+//   bounds[0] = max ||s_r b_r||_2, bounds[1] = max ||x_r - s_r b_r||_2 (rounded up; atomic max of
+//   the non-negative f64 bit patterns, so batches of adds accumulate).  Rows with max|x| < 1e-30
+//   are stored as b = 0 (scale 1): the whole row is residual.
+__global__ __launch_bounds__(256) void flat_ip_prepare_kernel(const float* __restrict__ xf, int64_t n,
+                                                              int8_t* __restrict__ x8,
+                                                              double* __restrict__ inv_scale,
+                                                              unsigned long long* __restrict__ bounds) {
+  __shared__ double sb[2][4];
+  const int w = threadIdx.x >> 6, l = lane_id();
+  const int64_t r = (int64_t)blockIdx.x * 4 + w;
+  double ex = 0.0, es = 0.0;
+  if (r < n) {
+    float xv[DPL];
+    load_q(xv, xf + r * DIM);
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) mx = fmaxf(mx, fabsf(xv[i]));
+#pragma unroll
+    for (int m = 1; m < WAVE; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
+    const bool live = mx >= 1e-30f;
+    const double sc = live ? (double)mx / 127.0 : 0.0, inv = live ? 127.0 / (double)mx : 0.0;
+    double b2 = 0.0, s2 = 0.0;
+    uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      double b = rint((double)xv[i] * inv);
+      b = b > 127.0 ? 127.0 : (b < -127.0 ? -127.0 : b);
+      const double rs = (double)xv[i] - sc * b;
+      b2 += b * b;
+      s2 += rs * rs;
+      pk[i >> 2] |= ((uint32_t)(int32_t)b & 0xffu) << (8 * (i & 3));
+    }
+    *reinterpret_cast<int4*>(x8 + r * DIM + DPL * l) = make_int4((int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]);
+    b2 = wave_sum_f64(b2);  // exact (integers < 2^24)
+    s2 = wave_sum_f64(s2);
+    ex = sc * sqrt(b2) * (1.0 + 1e-12);
+    es = sqrt(s2) * (1.0 + 1e-12) + 1e-300;
+    if (l == 0) inv_scale[r] = live ? inv : 1.0;
+  }
+  if (l == 0) {
+    sb[0][w] = ex;
+    sb[1][w] = es;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const double* v = sb[threadIdx.x];
+    const double m = fmax(fmax(v[0], v[1]), fmax(v[2], v[3]));
+    atomicMax(bounds + threadIdx.x, (unsigned long long)__double_as_longlong(m));
+  }
+}
+
 }  // namespace g5
 }  // namespace vrq
 
@@ -853,10 +924,101 @@ using namespace vrq::g5;
 
 extern "C" int vrq_gemm_topk_pieces(void) { return NPC; }
 
+namespace {
+
+bool gemm_mode_ok(int mode) {
+  return mode == VRQ_GEMM_BINARY || mode == VRQ_GEMM_INT8_COSINE || mode == VRQ_GEMM_FLOAT_IP;
+}
+
+template <int PH>
+void launch_finish(const Rows& c, int64_t n, int64_t row_offset, const float* qf, int nq, int k, const GemmPlan& p,
+                   const uint32_t* cand, const int32_t* cnt, int32_t* out_count, int64_t* out_rows,
+                   double* out_scores, int32_t* flag, bool fb, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_finish_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, cand, cnt,
+                     p.nchunks, p.capc, out_count, out_rows, out_scores, flag);
+  if (fb)
+    hipLaunchKernelGGL(gemm_fallback_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, out_count,
+                       out_rows, out_scores, (const int32_t*)flag);
+}
+
+// The three stages shared by every mode.  The matrix passes of VRQ_GEMM_FLOAT_IP are the int8
+// cosine passes over (the prepared int8 rows, 1/scale as the "norm"); only the prep kernel's bound
+// and the exact score differ.
+int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t row_offset, const float* qf, int nq,
+             int k, int flags, int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,
+             size_t workspace_bytes, hipStream_t s) {
+  GemmPlan p;
+  const int rc = gemm_plan(n, nq, k, &p);
+  if (rc != VRQ_OK) return rc;
+  if (workspace_bytes < p.bytes) return VRQ_EWORKSPACE;
+  constexpr int ALL = VRQ_GEMM_STAGE_SAMPLE | VRQ_GEMM_STAGE_MAIN | VRQ_GEMM_STAGE_FINISH;
+  const int st = (flags & ALL) ? (flags & ALL) : ALL;
+  uint8_t* ws = (uint8_t*)workspace;
+  int8_t* qa = (int8_t*)ws;
+  double* delta = (double*)(ws + p.off_delta);
+  float* thr = (float*)(ws + p.off_thr);
+  int32_t* flag = (int32_t*)(ws + p.off_flag);
+  int32_t* cnt = (int32_t*)(ws + p.off_cnt);
+  uint32_t* cand = (uint32_t*)(ws + p.off_cand);
+  float* dv = (float*)(ws + p.off_dv);
+  const bool P3 = mode != VRQ_GEMM_BINARY;  // int8 rows on the matrix cores
+  const uint8_t* src = P3 ? (const uint8_t*)c.x8 : c.codes;
+  const double* rn = c.norms;
+  const dim3 blk(GW * 64);
+  if (st & VRQ_GEMM_STAGE_SAMPLE) {
+    hipLaunchKernelGGL(gemm_prep_kernel, dim3((p.nq_pad + 3) / 4), dim3(256), 0, s, mode, qf, nq, p.nq_pad, qa,
+                       delta, bounds);
+    VRQ_LAUNCH_CHECK();
+    const dim3 grid(p.nsc * p.nqb);
+    if (P3)
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, true>), grid, blk, 0, s, src, rn, n, qa, nq,
+                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
+                         p.nqb, dv, p.scols);
+    else
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, true>), grid, blk, 0, s, src, rn, n, qa, nq,
+                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
+                         p.nqb, dv, p.scols);
+    VRQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, p.scr,
+                       p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq);
+    VRQ_LAUNCH_CHECK();
+  }
+  if (st & VRQ_GEMM_STAGE_MAIN) {
+    const dim3 grid(p.nchunks * p.nqb);
+    if (P3)
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, false>), grid, blk, 0, s, src, rn, n, qa, nq,
+                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                         (float*)nullptr, (int64_t)0);
+    else
+      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, false>), grid, blk, 0, s, src, rn, n, qa, nq,
+                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                         (float*)nullptr, (int64_t)0);
+    VRQ_LAUNCH_CHECK();
+  }
+  if (st & VRQ_GEMM_STAGE_FINISH) {
+    // VRQ_GEMM_FALLBACK=0 (tests only, read per call): skip the exact fallback, leaving flagged
+    // queries' outputs unwritten, to prove the matrix-core path alone served a batch
+    const char* fe = getenv("VRQ_GEMM_FALLBACK");
+    const bool fb = !(fe && fe[0] == '0');
+    if (mode == VRQ_GEMM_INT8_COSINE)
+      launch_finish<VRQ_GEMM_INT8_COSINE>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows,
+                                          out_scores, flag, fb, s);
+    else if (mode == VRQ_GEMM_FLOAT_IP)
+      launch_finish<VRQ_GEMM_FLOAT_IP>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows, out_scores,
+                                       flag, fb, s);
+    else
+      launch_finish<VRQ_GEMM_BINARY>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows, out_scores,
+                                     flag, fb, s);
+    VRQ_LAUNCH_CHECK();
+  }
+  return VRQ_OK;
+}
+
+}  // namespace
+
 extern "C" size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k) {
   GemmPlan p;
-  if ((mode != VRQ_GEMM_BINARY && mode != VRQ_GEMM_INT8_COSINE) || dim != DIM || gemm_plan(n, nq, k, &p) != VRQ_OK)
-    return 0;
+  if (!gemm_mode_ok(mode) || dim != DIM || gemm_plan(n, nq, k, &p) != VRQ_OK) return 0;
   return p.bytes;
 }
 
@@ -869,77 +1031,31 @@ extern "C" int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x
   VRQ_CHECK_ARG(qf && out_count && out_rows && out_scores && workspace && n > 0 && nq > 0 && k > 0);
   if (mode == VRQ_GEMM_BINARY) VRQ_CHECK_ARG(codes);
   if (mode == VRQ_GEMM_INT8_COSINE) VRQ_CHECK_ARG(x8 && norms);
-  GemmPlan p;
-  const int rc = gemm_plan(n, nq, k, &p);
-  if (rc != VRQ_OK) return rc;
-  if (workspace_bytes < p.bytes) return VRQ_EWORKSPACE;
-  constexpr int ALL = VRQ_GEMM_STAGE_SAMPLE | VRQ_GEMM_STAGE_MAIN | VRQ_GEMM_STAGE_FINISH;
-  const int st = (flags & ALL) ? (flags & ALL) : ALL;
-  hipStream_t s = (hipStream_t)stream;
-  uint8_t* ws = (uint8_t*)workspace;
-  int8_t* qa = (int8_t*)ws;
-  double* delta = (double*)(ws + p.off_delta);
-  float* thr = (float*)(ws + p.off_thr);
-  int32_t* flag = (int32_t*)(ws + p.off_flag);
-  int32_t* cnt = (int32_t*)(ws + p.off_cnt);
-  uint32_t* cand = (uint32_t*)(ws + p.off_cand);
-  float* dv = (float*)(ws + p.off_dv);
-  const bool P3 = mode == VRQ_GEMM_INT8_COSINE;
-  const uint8_t* src = P3 ? (const uint8_t*)x8 : codes;
-  const dim3 blk(GW * 64);
-  if (st & VRQ_GEMM_STAGE_SAMPLE) {
-    hipLaunchKernelGGL(gemm_prep_kernel, dim3((p.nq_pad + 3) / 4), dim3(256), 0, s, mode, qf, nq, p.nq_pad, qa,
-                       delta);
-    VRQ_LAUNCH_CHECK();
-    const dim3 grid(p.nsc * p.nqb);
-    if (P3)
-      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, true>), grid, blk, 0, s, src, norms, n, qa, nq,
-                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
-                         p.nqb, dv, p.scols);
-    else
-      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, true>), grid, blk, 0, s, src, norms, n, qa, nq,
-                         (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
-                         p.nqb, dv, p.scols);
-    VRQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, p.scr,
-                       p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq);
-    VRQ_LAUNCH_CHECK();
-  }
-  if (st & VRQ_GEMM_STAGE_MAIN) {
-    const dim3 grid(p.nchunks * p.nqb);
-    if (P3)
-      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, false>), grid, blk, 0, s, src, norms, n, qa, nq,
-                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
-                         (float*)nullptr, (int64_t)0);
-    else
-      hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, false>), grid, blk, 0, s, src, norms, n, qa, nq,
-                         (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
-                         (float*)nullptr, (int64_t)0);
-    VRQ_LAUNCH_CHECK();
-  }
-  if (st & VRQ_GEMM_STAGE_FINISH) {
-    // VRQ_GEMM_FALLBACK=0 (tests only, read per call): skip the exact fallback, leaving flagged
-    // queries' outputs unwritten, to prove the matrix-core path alone served a batch
-    const char* fe = getenv("VRQ_GEMM_FALLBACK");
-    const bool fb = !(fe && fe[0] == '0');
-    if (P3) {
-      hipLaunchKernelGGL(gemm_finish_kernel<VRQ_GEMM_INT8_COSINE>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
-                         row_offset, qf, k, (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count,
-                         out_rows, out_scores, flag);
-      VRQ_LAUNCH_CHECK();
-      if (fb)
-        hipLaunchKernelGGL(gemm_fallback_kernel<VRQ_GEMM_INT8_COSINE>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
-                         row_offset, qf, k, out_count, out_rows, out_scores, (const int32_t*)flag);
-    } else {
-      hipLaunchKernelGGL(gemm_finish_kernel<VRQ_GEMM_BINARY>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
-                         row_offset, qf, k, (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count,
-                         out_rows, out_scores, flag);
-      VRQ_LAUNCH_CHECK();
-      if (fb)
-        hipLaunchKernelGGL(gemm_fallback_kernel<VRQ_GEMM_BINARY>, dim3(nq), dim3(256), 0, s, codes, x8, norms, n,
-                         row_offset, qf, k, out_count, out_rows, out_scores, (const int32_t*)flag);
-    }
-    VRQ_LAUNCH_CHECK();
-  }
+  const Rows c{codes, x8, norms, nullptr};
+  return gemm_run(mode, c, nullptr, n, row_offset, qf, nq, k, flags, out_count, out_rows, out_scores, workspace,
+                  workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int vrq_flat_ip_prepare(const float* xf, int64_t n, int32_t dim, int8_t* x8, double* inv_scale,
+                                   double* bounds, void* stream) {
+  if (dim != DIM) return VRQ_EUNSUPPORTED;
+  VRQ_CHECK_ARG(n >= 0 && bounds);
+  if (n == 0) return VRQ_OK;
+  VRQ_CHECK_ARG(xf && x8 && inv_scale);
+  hipLaunchKernelGGL(flat_ip_prepare_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, xf, n,
+                     x8, inv_scale, reinterpret_cast<unsigned long long*>(bounds));
+  VRQ_LAUNCH_CHECK();
   return VRQ_OK;
+}
+
+extern "C" int vrq_flat_ip_topk(const float* xf, const int8_t* x8, const double* inv_scale, const double* bounds,
+                                int64_t n, int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k,
+                                int32_t flags, int32_t* out_count, int64_t* out_rows, double* out_scores,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  if (dim != DIM) return VRQ_EUNSUPPORTED;
+  VRQ_CHECK_ARG(xf && x8 && inv_scale && bounds && qf && out_count && out_rows && out_scores && workspace && n > 0 &&
+                nq > 0 && k > 0);
+  const Rows c{nullptr, x8, inv_scale, xf};
+  return gemm_run(VRQ_GEMM_FLOAT_IP, c, bounds, n, row_offset, qf, nq, k, flags, out_count, out_rows, out_scores,
+                  workspace, workspace_bytes, (hipStream_t)stream);
 }
