@@ -2,26 +2,29 @@
 """bench.py -- throughput of CohereEnhancedVectorDB's three-phase search on MI355X.
 
 Metric (BASELINE.json): queries/sec + recall@10 vs float32, d=1024 3-phase
-search at 1/2/4/8 GPUs.  Default workload = BASELINE config 2: 3-phase search
-over a 1M x 1024 synthetic corpus (SURVEY.md section 8(d) generator), query
-batches of nq = 1024, k = 10, binary_oversample = 10, int8_oversample = 3.
+search at 1/2/4/8 GPUs.  Default workload = BASELINE config 4: 3-phase search
+over a 100M x 1024 synthetic corpus (SURVEY.md section 8(d) generator), query
+batches of nq = 1024, k = 10, binary_oversample = 10, int8_oversample = 3.  The
+same corpus and the same batch at every N (strong scaling): with --gpus N the
+corpus is row-sharded over N ranks, each rank searches its shard and one RCCL
+all_gather + vrq_merge_shards reproduces the single-index result exactly.  At
+N = 1 the whole 100M-row corpus (codes 12.8 GB + int8 102.4 GB) sits in one
+MI355X's HBM.
 
 One step = one three-phase search of the whole nq-query batch:
   K1 vrq_search3_scan (Phase I Hamming scan, per-chunk exact top-K)
   K2 vrq_search3_finish (exact merge + Phase II + Phase III + stable sorts)
   [N > 1: one RCCL all_gather of the per-shard candidates + vrq_merge_shards]
-Inputs are HBM-resident before the timed region.  With --gpus N the 1M-row
-corpus is row-sharded over N ranks (strong scaling: the same corpus and the
-same query batch per step for every N); results are identical for every N.
+Inputs are HBM-resident before the timed region.
 
---config c3 runs the Phase-I-only HBM-roofline case instead (uniform random
-codes, queries = corpus rows with 64-256 flipped bits).
---config c5 runs BASELINE config 5: the batched Phase-II + Phase-III scoring of
-nq = 1024 queries against EVERY row of a 10M x 1024 corpus on the matrix cores
-(vrq_gemm_topk, int8-split queries x int8 / 0-1 rows on v_mfma_i32_32x32x32_i8),
-top-k fused; one step = both phases for the batch.
+--config c2  BASELINE config 2 (the same 3-phase search, 1M x 1024).
+--config c3  Phase-I-only HBM-roofline case (100M uniform random codes, queries
+             = corpus rows with 64-256 flipped bits, nq = 8 by default).
+--config c5  BASELINE config 5: the batched Phase-II + Phase-III scoring of
+             nq = 1024 queries against EVERY row of a 10M x 1024 corpus on the
+             matrix cores (vrq_gemm_topk), top-k fused.
 
-rank 0 prints ONE JSON line (see README of the driver contract).
+rank 0 prints ONE JSON line (the driver contract).
 """
 from __future__ import annotations
 
@@ -29,7 +32,6 @@ import argparse
 import ctypes
 import glob
 import json
-import math
 import os
 import sys
 import time
@@ -53,6 +55,18 @@ HBM_PEAK_GBS = 8000.0                          # MI355X spec (MI355X_MICROARCH.m
 VALU_PEAK_TOPS = 1024 * 64 / 4 * 2.4e9 / 1e12
 # dense FP4 MFMA peak (MI355X_MICROARCH.md: ~10 PF dense): 1024 SIMDs x 4096 ops/clk x 2.4 GHz
 MFMA_FP4_PEAK_TOPS = 1024 * 4096 * 2.4e9 / 1e12
+I8_DENSE_PEAK_TOPS = 1024 * 2048 * 2.4e9 / 1e12  # v_mfma_i32_32x32x32_i8: 32 cycles, 2x the bf16 rate
+
+# workload of each --config: corpus rows, queries per step, Phase-I only
+CONFIGS = {
+    "c4": dict(n=100_000_000, nq=1024, phase1=False,
+               name="BASELINE config 4: CohereEnhancedVectorDB 3-phase search, row-sharded over N GPUs + RCCL "
+                    "all_gather of per-shard top-K"),
+    "c2": dict(n=1_000_000, nq=1024, phase1=False, name="BASELINE config 2: CohereEnhancedVectorDB 3-phase search"),
+    "c3": dict(n=100_000_000, nq=8, phase1=True, name="BASELINE config 3: Phase-I-only Hamming top-k"),
+    "c5": dict(n=10_000_000, nq=1024, phase1=False, name="BASELINE config 5: batched Phase-II + Phase-III exhaustive "
+                                                          "scoring"),
+}
 
 
 def parse():
@@ -60,17 +74,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c4")
     ap.add_argument("--n", type=int, default=None, help="corpus rows (total over all ranks)")
     ap.add_argument("--nq", type=int, default=None, help="queries per step")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--binary-oversample", type=int, default=10)
     ap.add_argument("--int8-oversample", type=int, default=3)
-    ap.add_argument("--cpu-sample", type=int, default=1024, help="queries per pass of the host CPU baseline")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="queries per pass of the host CPU baseline (default: sized to ~10 s of CPU work)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="host threads of the CPU baseline (default: OMP_NUM_THREADS, else os.cpu_count())")
     ap.add_argument("--recall-sample", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
+    ap.add_argument("--no-encode", action="store_true", help="skip the encoder roofline leg")
     ap.add_argument("--scan", choices=["auto", "valu", "mfma"], default="auto",
                     help="Phase-I scan (auto = the library's choice for the shape)")
     return ap.parse_args()
@@ -78,6 +95,28 @@ def parse():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def host_info(threads):
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cores": threads, "host_nproc": os.cpu_count(), "cpu_model": model,
+            "cores_note": "threads the baseline ran on = the box's CPU share for one GPU (OMP_NUM_THREADS); "
+                          "host_nproc is the whole machine"}
+
+
+def cpu_threads(a):
+    if a.cpu_threads:
+        return a.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return int(env) if env.isdigit() and int(env) > 0 else (os.cpu_count() or 1)
 
 
 class Pipeline:
@@ -107,7 +146,6 @@ class Pipeline:
         self.prefix_rows = int(pre.value)
         ws = self.lib.vrq_search3_workspace_size(self.m, 1024, nq, self.K)
         self.ws = torch.empty((max(ws, 8),), dtype=torch.uint8, device=dev)
-        self.list_bytes = ws
         kout = self.K if self.flags & (N.VRQ_SEARCH_SHARD | N.VRQ_SEARCH_PHASE1_ONLY) else k
         self.cnt = torch.empty((nq,), dtype=torch.int32, device=dev)
         self.rows = torch.empty((nq, kout), dtype=torch.int64, device=dev)
@@ -196,30 +234,66 @@ def recall_at_10(top_rows, qf, n_total, rank, world, dev, sample):
     return float(np.mean([len(set(a[a >= 0]) & set(b)) / 10.0 for a, b in zip(got, gt)]))
 
 
-def cpu_baseline(codes_h, x8_h, qf_h, qb_h, k, osb, osi, threads, sample, gpu_rows=None, min_s=10.0,
-                 single_sample=32):
-    """Restated reference path on the host: FAISS hammings_knn_hc in C (OpenMP over queries)
-    + the reference's NumPy Phase II / III per query.  Returns (dict, parity_ok)."""
-    import ctypes as C
+def real_data_recall(dev):
+    """The same GPU search on the reference's persisted 1000-document Cohere corpus (golden fixture
+    tests/golden/search_real.npz: codes from its index.bin, int8 from its RocksDB SST, queries = 100 doc float
+    vectors): recall@10 vs exact float32 IP, and agreement of the top-10 ids with the reference's own
+    CohereEnhancedVectorDB.search output on that data."""
+    from vectorragquantization_amd.enhanced import search3
+    from vectorragquantization_amd.quant import int8_row_norms
+    p = os.path.join(HERE, "tests", "golden", "search_real.npz")
+    if not os.path.exists(p):
+        return None
+    g = np.load(p)
+    codes = torch.from_numpy(g["codes"]).to(dev)
+    x8 = torch.from_numpy(g["int8"]).to(dev)
+    qf = torch.from_numpy(g["qf"]).to(dev)
+    qb = torch.from_numpy(g["qb"]).to(dev)
+    cnt, rows, _, _, _ = search3(codes, x8, int8_row_norms(x8), qf, qb, 10, 100, 30)
+    got = rows.cpu().numpy()
+    gt = g["gt_float_top10"]
+    rec = float(np.mean([len(set(a[a >= 0]) & set(b)) / 10.0 for a, b in zip(got, gt)]))
+    same = float(np.mean([np.array_equal(a, b) for a, b in zip(got, g["k10_ids"])]))
+    return {"recall_at_10": rec, "reference_top10_identical": same, "queries": int(got.shape[0]),
+            "corpus": "reference db_cohere_enhanced (1000 real Cohere embed-english-v3.0 docs)"}
+
+
+def _oracle_lib():
     import subprocess
-    from oracle import oracle_np as O
     so = os.path.join(HERE, "oracle", "_build", "liboracle.so")
     if not os.path.exists(so):
         subprocess.check_call([os.path.join(HERE, "oracle", "build.sh")])
-    lib = C.CDLL(so)
-    lib.oracle_hamming_knn.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int, C.c_int,
-                                       C.c_void_p, C.c_void_p, C.c_int]
+    lib = ctypes.CDLL(so)
+    lib.oracle_hamming_knn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    return lib
+
+
+def cpu_phase1(lib, codes_h, qb, K, nthreads):
+    """FAISS hammings_knn_hc restatement (C, OpenMP over queries): (D i32[nq, K], I i64[nq, K])."""
+    qb = np.ascontiguousarray(qb)
+    D = np.empty((qb.shape[0], K), np.int32)
+    I = np.empty((qb.shape[0], K), np.int64)
+    lib.oracle_hamming_knn(codes_h.ctypes.data, codes_h.shape[0], 128, qb.ctypes.data, qb.shape[0], K,
+                           D.ctypes.data, I.ctypes.data, nthreads)
+    return D, I
+
+
+def cpu_baseline(codes_h, fetch_x8, qf_h, qb_h, k, osb, osi, threads, sample, gpu_rows=None, min_s=10.0,
+                 single_sample=32):
+    """Restated reference path on the host: FAISS hammings_knn_hc in C (OpenMP over queries)
+    + the reference's NumPy Phase II / III per query (CohereEnhancedVectorDB.py:281-322).
+
+    ``fetch_x8(rows)`` returns the int8 rows of the given candidates: the reference fetches each
+    Phase-III candidate from its RocksDB store (:303); here they are fetched from the device copy
+    between the timed Phase I and the timed Phases II/III (not timed, like the reference's HTTP).
+    Returns (dict, top-10 agreement with the GPU)."""
+    from oracle import oracle_np as O  # noqa: F401  (checker module; keeps the import path explicit)
+    lib = _oracle_lib()
     nq = min(sample, qf_h.shape[0])
     K = min(k * osb, codes_h.shape[0])
 
-    def phase1(qb, nthreads):
-        D = np.empty((qb.shape[0], K), np.int32)
-        I = np.empty((qb.shape[0], K), np.int64)
-        lib.oracle_hamming_knn(codes_h.ctypes.data, codes_h.shape[0], 128, qb.ctypes.data, qb.shape[0], K,
-                               D.ctypes.data, I.ctypes.data, nthreads)
-        return I
-
-    def phase23(q, rows):
+    def phase23(q, rows, x8_of):
         rows = rows[rows >= 0]
         pm = 2 * np.unpackbits(codes_h[rows], axis=1).astype(np.int32) - 1
         s2 = pm.astype(np.float64) @ qf_h[q].astype(np.float64)
@@ -227,11 +301,16 @@ def cpu_baseline(codes_h, x8_h, qf_h, qb_h, k, osb, osi, threads, sample, gpu_ro
         r3 = rows[o2]
         s3 = []
         for r in r3:
-            v = x8_h[r]
+            v = x8_of[int(r)]
             nrm = np.linalg.norm(v)
             s3.append(-np.inf if nrm == 0 else float(qf_h[q].dot(v)) / nrm)
         o3 = sorted(range(len(s3)), key=lambda j: -s3[j])[:k]
         return r3[o3]
+
+    def fetch(I):
+        u = np.unique(I[I >= 0])
+        X = fetch_x8(u)
+        return {int(r): X[i] for i, r in enumerate(u)}
 
     # all host threads given: the whole sample per pass, passes repeated until ~min_s of CPU work
     qb = np.ascontiguousarray(qb_h[:nq])
@@ -239,32 +318,97 @@ def cpu_baseline(codes_h, x8_h, qf_h, qb_h, k, osb, osi, threads, sample, gpu_ro
     reps = 0
     while True:
         t0 = time.perf_counter()
-        I = phase1(qb, threads)
+        _, I = cpu_phase1(lib, codes_h, qb, K, threads)
         t1 = time.perf_counter()
-        out_rows = [phase23(q, I[q]) for q in range(nq)]
+        x8_of = fetch(I)
         t2 = time.perf_counter()
-        t_p1, t_p23, reps = t_p1 + t1 - t0, t_p23 + t2 - t1, reps + 1
+        out_rows = [phase23(q, I[q], x8_of) for q in range(nq)]
+        t3 = time.perf_counter()
+        t_p1, t_p23, reps = t_p1 + t1 - t0, t_p23 + t3 - t2, reps + 1
         if t_p1 + t_p23 >= min_s or reps >= 50:
             break
     # one core, one query per call: the reference's own behaviour (FAISS parallelises over queries only)
     n1 = min(single_sample, nq)
-    t0 = time.perf_counter()
+    t_single = 0.0
     for q in range(n1):
-        phase23(q, phase1(np.ascontiguousarray(qb_h[q:q + 1]), 1)[0])
-    t_single = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        _, I1 = cpu_phase1(lib, codes_h, qb_h[q:q + 1], K, 1)
+        t1 = time.perf_counter()
+        x8_of = fetch(I1)
+        t2 = time.perf_counter()
+        phase23(q, I1[0], x8_of)
+        t_single += t1 - t0 + time.perf_counter() - t2
     parity = None
     if gpu_rows is not None:
         g = gpu_rows[:nq]
-        parity = float(np.mean([len(set(a) & set(b[b >= 0])) / max(1, len(a)) for a, b in zip(out_rows, g)]))
+        parity = float(np.mean([np.array_equal(a, b[b >= 0]) for a, b in zip(out_rows, g)]))
     qps = nq * reps / (t_p1 + t_p23)
-    return {"value": qps, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{nq} queries of the same batch over the full {codes_h.shape[0]}-row corpus, {reps} passes; "
-                      f"Phase I = C restatement of FAISS hammings_knn_hc (OpenMP over queries, {threads} threads, "
-                      f"{t_p1:.2f} s), Phases II/III = the reference NumPy per-query code (1 thread, "
-                      f"{t_p23:.2f} s). FAISS itself is not available offline.",
-            "phase1_s": t_p1, "phase23_s": t_p23,
-            "single_core": {"value": n1 / t_single, "unit": "queries/s", "cores": 1,
-                            "sample": f"{n1} queries, one per call (nq=1), Phase I on 1 thread + NumPy II/III"}}, parity
+    out = {"value": qps, "unit": "queries/s", "kind": "port", **host_info(threads),
+           "sample": f"{nq} queries of the same batch over the full {codes_h.shape[0]}-row corpus, {reps} pass(es); "
+                     f"Phase I = C restatement of FAISS hammings_knn_hc (OpenMP over queries, {threads} threads, "
+                     f"{t_p1:.2f} s), Phases II/III = the reference NumPy per-query code (1 thread, {t_p23:.2f} s; "
+                     "candidate int8 rows fetched untimed, as the reference's RocksDB gets). FAISS itself is not "
+                     "available offline.",
+           "phase1_s": t_p1, "phase23_s": t_p23,
+           "single_core": {"value": n1 / t_single, "unit": "queries/s", "cores": 1,
+                           "sample": f"{n1} queries, one per call (nq=1), Phase I on 1 thread + NumPy II/III"}}
+    return out, parity
+
+
+def cpu_baseline_phase1(codes_h, qb_h, K, threads, gpu_dist, gpu_rows, min_s=10.0):
+    """Config 3 baseline: the FAISS hammings_knn_hc restatement over the same queries and corpus, timed on the
+    host; and the identity check of the GPU's Phase-I output against it (every (dist, row) of the top-K and
+    the top-10 ids)."""
+    lib = _oracle_lib()
+    nq = qb_h.shape[0]
+    t, reps = 0.0, 0
+    D = I = None
+    while t < min_s and reps < 20:
+        t0 = time.perf_counter()
+        D, I = cpu_phase1(lib, codes_h, qb_h, K, threads)
+        t += time.perf_counter() - t0
+        reps += 1
+    t0 = time.perf_counter()
+    cpu_phase1(lib, codes_h, qb_h[:1], K, 1)
+    t1q = time.perf_counter() - t0
+    ident_k = bool(np.array_equal(D, gpu_dist) and np.array_equal(I, gpu_rows))
+    ident_10 = float(np.mean([np.array_equal(a[:10], b[:10]) for a, b in zip(I, gpu_rows)]))
+    return {"value": nq * reps / t, "unit": "queries/s", "kind": "port", **host_info(threads),
+            "sample": f"the same {nq} queries over the full {codes_h.shape[0]}-row corpus, {reps} pass(es), C "
+                      f"restatement of FAISS hammings_knn_hc (OpenMP over queries, {threads} threads, {t:.2f} s)",
+            "single_core": {"value": 1.0 / t1q, "unit": "queries/s", "cores": 1, "sample": "1 query (nq=1), 1 thread"},
+            }, {"topK_dist_rows_identical": ident_k, "top10_ids_identical": ident_10}
+
+
+def encode_roofline(dev, n=1 << 20, reps=5):
+    """vrq_encode over n f32 vectors per mode against the HBM roofline (SURVEY.md 8(d) encode row).
+    Algorithmic bytes per vector: the input row (4096 B f32 / 2048 B i16) + the code row (128 B) + the
+    quantised row (1024 / 2048 / 512 B) + min/max (16 B, local modes)."""
+    from vectorragquantization_amd.quant import encode
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    X = torch.randn((n, 1024), generator=g, device=dev) * 0.05
+    X16 = (X * 3000).to(torch.int16)
+    qbytes = {"int8g": 1024, "int16g": 2048, "int4g": 512, "int8": 1024 + 16, "int4": 512 + 16, "bin16": 0,
+              "cohere": 1024}
+    out = {}
+    for mode in ("int8g", "int16g", "int4g", "int8", "int4", "bin16", "cohere"):
+        inp = X16 if mode == "bin16" else X
+        encode(mode, inp, 0.1, dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            encode(mode, inp, 0.1, dev)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        b = n * ((2048 if mode == "bin16" else 4096) + 128 + qbytes[mode])
+        out[mode] = {"ms": ms, "GB/s": b / (ms * 1e-3) / 1e9, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "bytes_per_launch": b}
+    del X, X16
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "vectors_per_launch": n,
+            "timing": "HIP events around 5 launches (includes the host-side output allocation)", "modes": out}
 
 
 def pmc_traffic(tag, kernel):
@@ -288,9 +432,6 @@ def measured_mfma_peak():
         return float(d["mfma_scale_f32_32x32x64_fp4"]["TOPS"])
     except Exception:
         return None
-
-
-I8_DENSE_PEAK_TOPS = 1024 * 2048 * 2.4e9 / 1e12  # v_mfma_i32_32x32x32_i8: 32 cycles, 2x the bf16 rate
 
 
 class C5Pipeline:
@@ -363,21 +504,12 @@ def cpu_baseline_c5(codes_h, x8_h, qf_h, k, n, nq_s=4, threads=16):
                                                     x8=x8_h[a:a + 65536]) for a in range(0, rs, 65536)], 1)
             O.exhaustive_topk(S, k)
     t = time.perf_counter() - t0
-    return {"value": nq_s / (t * n / rs), "unit": "queries/s", "cores": threads, "kind": "port",
+    return {"value": nq_s / (t * n / rs), "unit": "queries/s", "kind": "port", **host_info(threads),
             "sample": f"{nq_s} queries x the first {rs} of {n} rows, both phases (NumPy float64 GEMV over "
                       f"2*unpackbits-1; float32 dot / float64 norm), {t:.1f} s, scaled by n/{rs}"}
 
 
-def run_c5(a, world, rank, dev):
-    n = a.n or 10_000_000
-    nq = a.nq or 1024
-    t_setup = time.perf_counter()
-    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
-    codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
-    qf, qb, _ = synth.make_queries(n, nq, device=dev)
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] c5 data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
-    P = C5Pipeline(codes, x8, norms, row0, qf, a.k, world)
+def timed_loop(P, a, world, dev):
     for _ in range(a.warmup):
         P.step(False)
     torch.cuda.synchronize()
@@ -395,6 +527,20 @@ def run_c5(a, world, rank, dev):
         tt = torch.tensor([T], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
+    return T
+
+
+def run_c5(a, world, rank, dev):
+    n = a.n or CONFIGS["c5"]["n"]
+    nq = a.nq or CONFIGS["c5"]["nq"]
+    t_setup = time.perf_counter()
+    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+    codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
+    qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] c5 data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
+    P = C5Pipeline(codes, x8, norms, row0, qf, a.k, world)
+    T = timed_loop(P, a, world, dev)
     rec = None
     if not a.no_recall:
         rec = recall_at_10(P.final[3][1], qf, n, rank, world, dev, min(a.recall_sample, nq))
@@ -425,8 +571,8 @@ def run_c5(a, world, rank, dev):
         "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "i8 (int8-quantised f32 queries, proven error bound) + f64 exact rescoring",
         "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)",
-        "config": {"workload": f"BASELINE config 5: batched Phase-II + Phase-III exhaustive scoring, {n} x 1024 "
-                               f"corpus, nq={nq} queries per step, fused top-{a.k}",
+        "config": {"workload": f"{CONFIGS['c5']['name']}, {n} x 1024 corpus, nq={nq} queries per step, "
+                               f"fused top-{a.k}",
                    "corpus_rows": n, "nq": nq, "k": a.k,
                    "parallelism": f"row-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU"},
         "recall_at_10": rec, "phase_ms": st, "roofline": roof, "roofline_binary": roof_bin,
@@ -434,7 +580,7 @@ def run_c5(a, world, rank, dev):
     if world == 1 and not a.no_cpu_baseline:
         rs = min(m, 1_000_000)
         out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
-                                              a.k, m, threads=a.cpu_threads)
+                                              a.k, m, threads=cpu_threads(a))
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -453,9 +599,10 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     if a.config == "c5":
         return run_c5(a, world, rank, dev)
-    phase1 = a.config == "c3"
-    n = a.n or (100_000_000 if phase1 else 1_000_000)
-    nq = a.nq or (8 if phase1 else 1024)
+    cfg = CONFIGS[a.config]
+    phase1 = cfg["phase1"]
+    n = a.n or cfg["n"]
+    nq = a.nq or cfg["nq"]
     N.load()
     t_setup = time.perf_counter()
     if phase1:
@@ -477,23 +624,7 @@ def main():
 
     P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, phase1,
                  a.scan)
-    for _ in range(a.warmup):
-        P.step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        P.step(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    T = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([T], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        T = float(tt.item())
+    T = timed_loop(P, a, world, dev)
 
     top_rows = P.final[1]
     rec = None
@@ -541,24 +672,44 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "u8" if phase1 else "u8+f64",
         "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)"
                 if not phase1 else "synthetic (uniform random 1024-bit codes, bit-flipped-row queries)",
-        "config": {"workload": ("BASELINE config 3: Phase-I-only Hamming top-k" if phase1 else
-                                "BASELINE config 2: CohereEnhancedVectorDB 3-phase search") +
-                               f", {n} x 1024 corpus, nq={nq} queries per step",
-                   "corpus_rows": n, "nq": nq, "k": a.k, "binary_oversample": a.binary_oversample,
+        "config": {"workload": f"{cfg['name']}, {n} x 1024 corpus, nq={nq} queries per step",
+                   "corpus_rows": n, "rows_per_gpu": m, "nq": nq, "k": a.k, "binary_oversample": a.binary_oversample,
                    "int8_oversample": a.int8_oversample, "parallelism": f"row-shard x{world} + RCCL all_gather"
                    if world > 1 else "1 GPU"},
         "recall_at_10": rec,
         "phase_ms": st, "scan_kind": "mfma" if P.kind == N.VRQ_SCAN_KIND_MFMA else "valu",
         "roofline": roof, "roofline_scan_hbm": roof_scan_hbm, "roofline_valu": roof_valu,
     }
+    if not phase1 and not a.no_recall:
+        out["recall_note"] = ("recall_at_10 is vs exact float32 IP over the synthetic generator's floats; its "
+                              "top-10 beyond the query's source row is a near-tie among ~n/4096 cluster-mates, which "
+                              "sign-bit codes cannot resolve (the CPU path agrees exactly). real_data is the same "
+                              "GPU search on the reference's own persisted Cohere corpus.")
+        out["real_data"] = real_data_recall(dev)
+    threads = cpu_threads(a)
     if world == 1 and not a.no_cpu_baseline and not phase1:
-        cb, parity = cpu_baseline(codes.cpu().numpy(), x8.cpu().numpy(), qf.cpu().numpy(), qb.cpu().numpy(),
-                                  a.k, a.binary_oversample, a.int8_oversample, a.cpu_threads, a.cpu_sample,
-                                  top_rows.cpu().numpy())
+        sample = a.cpu_sample or (1024 if n <= 2_000_000 else 64)
+        x8_src = x8
+
+        def fetch_x8(rows):
+            return x8_src[torch.from_numpy(rows).to(dev)].cpu().numpy()
+        t0 = time.perf_counter()
+        codes_h = codes.cpu().numpy()
+        log(f"[rank 0] codes to host in {time.perf_counter() - t0:.1f} s; CPU baseline on {threads} threads, "
+            f"{sample} queries")
+        cb, parity = cpu_baseline(codes_h, fetch_x8, qf.cpu().numpy(), qb.cpu().numpy(), a.k, a.binary_oversample,
+                                  a.int8_oversample, threads, sample, top_rows.cpu().numpy(),
+                                  single_sample=max(2, min(32, 400_000_000 // n)))
         out["cpu_baseline"] = cb
-        out["cpu_gpu_top10_agreement"] = parity
+        out["cpu_gpu_top10_identical"] = parity
+        del codes_h
     elif world == 1 and not a.no_cpu_baseline and phase1:
-        out["cpu_baseline"] = None
+        cb, ident = cpu_baseline_phase1(codes.cpu().numpy(), qb.cpu().numpy(), K, threads,
+                                        P.dist.cpu().numpy(), P.rows.cpu().numpy())
+        out["cpu_baseline"] = cb
+        out["cpu_gpu_identity"] = ident
+    if world == 1 and not phase1 and not a.no_encode:
+        out["roofline_encode"] = encode_roofline(dev)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

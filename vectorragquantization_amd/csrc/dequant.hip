@@ -111,9 +111,18 @@ int vrq_dequantize(int32_t mode, const void* q, const double* minmax, int64_t n,
   if (n == 0) return VRQ_OK;
   VRQ_CHECK_ARG(q && out);
   if (mode == VRQ_ENC_INT8_LOCAL || mode == VRQ_ENC_INT4_LOCAL) VRQ_CHECK_ARG(minmax);
-  hipLaunchKernelGGL(dequant_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, (int)mode, q, minmax, n,
-                     (int)dim, limit, out);
-  VRQ_LAUNCH_CHECK();
+  // one workgroup per row; launches of at most 2^22 rows keep a dispatch below 2^32 work-items
+  const int64_t qrow = mode == VRQ_ENC_INT16_GLOBAL                              ? 2 * (int64_t)dim
+                       : (mode == VRQ_ENC_INT4_GLOBAL || mode == VRQ_ENC_INT4_LOCAL) ? (int64_t)(dim + 1) / 2
+                                                                                    : (int64_t)dim;
+  constexpr int64_t kMaxLaunch = 1 << 22;
+  for (int64_t r0 = 0; r0 < n; r0 += kMaxLaunch) {
+    const int64_t nr = n - r0 < kMaxLaunch ? n - r0 : kMaxLaunch;
+    hipLaunchKernelGGL(dequant_kernel, dim3((unsigned)nr), dim3(256), 0, (hipStream_t)stream, (int)mode,
+                       (const void*)((const uint8_t*)q + r0 * qrow), minmax ? minmax + 2 * r0 : nullptr, nr, (int)dim,
+                       limit, out + r0 * dim);
+    VRQ_LAUNCH_CHECK();
+  }
   return VRQ_OK;
 }
 

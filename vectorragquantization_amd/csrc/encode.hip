@@ -224,26 +224,29 @@ __global__ __launch_bounds__(64) void encode_kernel(const void* __restrict__ xin
 // K7: ||x8 row||_2 in float64 from the exact integer sum of squares.
 __global__ __launch_bounds__(256) void int8_norms_kernel(const int8_t* __restrict__ x8, int64_t n, int dim,
                                                          double* __restrict__ out) {
-  const int64_t v = ((int64_t)blockIdx.x * 256 + threadIdx.x) / WAVE;
-  if (v >= n) return;
+  // grid-stride over rows, one wave per row: the grid stays far below the 2^32 work-item limit of a
+  // dispatch at 100M rows
+  const int64_t nw = (int64_t)gridDim.x * 4;
   const int l = lane_id();
-  const int8_t* r = x8 + v * dim;
-  int64_t s = 0;
-  if ((dim & 15) == 0) {
-    for (int i = 16 * l; i < dim; i += 16 * WAVE) {
-      const int4 raw = *reinterpret_cast<const int4*>(r + i);
-      const int32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  for (int64_t v = ((int64_t)blockIdx.x * 256 + threadIdx.x) / WAVE; v < n; v += nw) {
+    const int8_t* r = x8 + v * dim;
+    int64_t s = 0;
+    if ((dim & 15) == 0) {
+      for (int i = 16 * l; i < dim; i += 16 * WAVE) {
+        const int4 raw = *reinterpret_cast<const int4*>(r + i);
+        const int32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int32_t e = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
-        s += e * e;
+        for (int k = 0; k < 16; ++k) {
+          const int32_t e = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+          s += e * e;
+        }
       }
+    } else {
+      for (int i = l; i < dim; i += WAVE) s += (int32_t)r[i] * (int32_t)r[i];
     }
-  } else {
-    for (int i = l; i < dim; i += WAVE) s += (int32_t)r[i] * (int32_t)r[i];
+    s = wave_sum_i64(s);
+    if (l == 0) out[v] = sqrt((double)s);
   }
-  s = wave_sum_i64(s);
-  if (l == 0) out[v] = sqrt((double)s);
 }
 
 }  // namespace vrq
@@ -281,31 +284,44 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
   if (P.nleaves > MAX_LEAVES) return VRQ_EUNSUPPORTED;
   const size_t lds = sizeof(float) * (dim + 2 * MAX_LEAVES);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)n), block(64);
-  switch (mode) {
-    case VRQ_ENC_INT8_GLOBAL:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    case VRQ_ENC_INT16_GLOBAL:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    case VRQ_ENC_INT4_GLOBAL:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    case VRQ_ENC_INT8_LOCAL:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    case VRQ_ENC_INT4_LOCAL:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    case VRQ_ENC_BIN_INT16:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_BIN_INT16>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
-    default:
-      hipLaunchKernelGGL(encode_kernel<VRQ_ENC_COHERE>, grid, block, lds, s, x, n, dim, limit, codes, q, minmax, P);
-      break;
+  // one wave per vector; launches of at most 2^24 vectors keep a dispatch below 2^32 work-items
+  const int64_t xrow = (int64_t)dim * (mode == VRQ_ENC_BIN_INT16 ? 2 : 4);
+  const int64_t qrow = mode == VRQ_ENC_INT16_GLOBAL                              ? 2 * (int64_t)dim
+                       : (mode == VRQ_ENC_INT4_GLOBAL || mode == VRQ_ENC_INT4_LOCAL) ? (int64_t)(dim + 1) / 2
+                                                                                    : (int64_t)dim;
+  constexpr int64_t kMaxLaunch = 1 << 24;
+  for (int64_t v0 = 0; v0 < n; v0 += kMaxLaunch) {
+    const int64_t nv = n - v0 < kMaxLaunch ? n - v0 : kMaxLaunch;
+    const void* xv = (const uint8_t*)x + v0 * xrow;
+    uint8_t* cv = codes + v0 * (dim / 8);
+    void* qv = q ? (void*)((uint8_t*)q + v0 * qrow) : nullptr;
+    double* mv = minmax ? minmax + 2 * v0 : nullptr;
+    const dim3 grid((unsigned)nv), block(64);
+    switch (mode) {
+      case VRQ_ENC_INT8_GLOBAL:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      case VRQ_ENC_INT16_GLOBAL:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      case VRQ_ENC_INT4_GLOBAL:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      case VRQ_ENC_INT8_LOCAL:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      case VRQ_ENC_INT4_LOCAL:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      case VRQ_ENC_BIN_INT16:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_BIN_INT16>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+      default:
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_COHERE>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        break;
+    }
+    VRQ_LAUNCH_CHECK();
   }
-  VRQ_LAUNCH_CHECK();
   return VRQ_OK;
 }
 
@@ -313,7 +329,8 @@ int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, vo
   VRQ_CHECK_ARG(n >= 0 && dim > 0);
   if (n == 0) return VRQ_OK;
   VRQ_CHECK_ARG(x8 && out);
-  const int64_t blocks = (n * WAVE + 255) / 256;
+  int64_t blocks = (n * WAVE + 255) / 256;
+  if (blocks > (1 << 20)) blocks = 1 << 20;  // 4M waves, grid-stride beyond
   hipLaunchKernelGGL(int8_norms_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x8, n, dim, out);
   VRQ_LAUNCH_CHECK();
   return VRQ_OK;
