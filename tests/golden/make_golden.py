@@ -32,11 +32,18 @@ Safe loading: index.bin / index.faiss are raw FAISS binary formats read with
 nothing) is used to pull out the ``"doc"`` string and the raw 1024-byte int8
 payload.
 
-* ``CohereVectorDBFloat.add_documents/remove_document/search`` (``:103-180``) on the
-  reference's persisted float data (faiss's IndexIDMap(IndexFlatIP) = the oracle
-  restatement) -> ``flat_real.npz``.
+* ``CohereVectorDBFloat.add_documents/remove_document/search`` (``:103-180``) run on the
+  reference's persisted float data -> ``flat_real.npz``.  ``faiss.IndexIDMap(IndexFlatIP)``
+  there is the oracle's restatement (f64 sum rounded once to f32, ties by row ascending), so
+  the labels, order and scores pin the reference's Python around FAISS plus that restatement;
+  FAISS's own f32 ``fvec_inner_product`` rounding and heap tie order are "parity unpinned".
+  Only the ``index.faiss`` bytes (sha256) are the reference's own output.
+* ``ref_db/``: byte copies of persisted reference DATA files (FAISS index.bin, config.json and
+  the RocksDB SST tables of ``db_cohere_enhanced``, ``db_cohere_float`` and ``db_int4_global``
+  -- the last one Snappy-compressed), so tests can open reference folders with the product's
+  RocksDict reader on a box where /root/reference does not exist.
 
-Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real|flat_real ...]
+Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real|flat_real|ref_db ...]
 """
 from __future__ import annotations
 
@@ -471,6 +478,21 @@ def gen_flat_real(out_path: str):
     print("wrote", out_path)
 
 
+def gen_ref_db(out_dir: str):
+    """Byte copies of persisted reference data files (no source): the folders tests open."""
+    import shutil
+    files = ["db_cohere_enhanced/config.json", "db_cohere_enhanced/index.bin", "db_cohere_enhanced/docs/000009.sst",
+             "db_cohere_enhanced/docs/CURRENT", "db_cohere_float/config.json", "db_cohere_float/docs/000009.sst",
+             "db_cohere_float/docs/CURRENT", "db_int4_global/config.json", "db_int4_global/index.bin",
+             "db_int4_global/docs/000009.sst", "db_int4_global/docs/CURRENT"]
+    for f in files:
+        dst = os.path.join(out_dir, f)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(os.path.join(REF, f), dst)
+        os.chmod(dst, 0o644)
+    print("wrote", out_dir)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference checkout not mounted; fixtures are generated in the build container only")
@@ -485,3 +507,5 @@ if __name__ == "__main__":
         gen_search_real(os.path.join(HERE, "search_real.npz"))
     if not only or "flat_real" in only:
         gen_flat_real(os.path.join(HERE, "flat_real.npz"))
+    if not only or "ref_db" in only:
+        gen_ref_db(os.path.join(HERE, "ref_db"))

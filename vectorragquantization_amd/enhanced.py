@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from .docstore import DocStoreError, RocksDictReader, is_rocksdict_dir
 from .index import BinaryIndexIDMap2, _GrowBuffer, as_device_tensor
 from .quant import int8_row_norms
 
@@ -83,6 +84,9 @@ def gemm_topk(mode: str, qf: torch.Tensor, k: int, codes: torch.Tensor | None = 
     N.check(lib.vrq_gemm_topk(m, N.ptr(codes), N.ptr(x8), N.ptr(norms), n, qf.shape[1], row_offset, N.ptr(qf), nq,
                               k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores), N.ptr(workspace),
                               workspace.numel(), N.stream_handle(dev)), "vrq_gemm_topk")
+    if os.environ.get("VRQ_GEMM_FALLBACK") == "0" and bool((cnt < 0).any()):
+        # test hook: the library skipped the exact fallback and left the flagged queries unwritten
+        raise N.VrqNativeError("vrq_gemm_topk: queries needed the exact fallback, which VRQ_GEMM_FALLBACK=0 disabled")
     return cnt, rows, scores
 
 
@@ -100,6 +104,11 @@ def search3(codes: torch.Tensor, x8: torch.Tensor, norms: torch.Tensor, qf: torc
     dist = torch.empty((nq, kout), dtype=torch.int32, device=dev)
     s2 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
     s3 = torch.empty((nq, kout), dtype=torch.float64, device=dev)
+    if not flags & N.VRQ_SEARCH_PHASE1_ONLY and n and (x8.shape[0] != n or norms.shape[0] != n):
+        # the ABI indexes x8 / norms by code row and cannot see their lengths
+        raise N.VrqNativeError(f"vrq_search3: {n} code rows but {x8.shape[0]} int8 rows and {norms.shape[0]} norms")
+    if rescore_row is not None and rescore_row.shape[0] != n:
+        raise N.VrqNativeError(f"vrq_search3: rescore_row has {rescore_row.shape[0]} entries for {n} rows")
     lib = N.load()
     need = lib.vrq_search3_workspace_size(n, dim, nq, K) if n and nq and K else 0
     if workspace is None or workspace.numel() < need:
@@ -163,23 +172,73 @@ class CohereEnhancedVectorDB:
         self.config = config
 
     def _docs_path(self):
-        return os.path.join(self.folder, "docs")
+        """This build's document store (int8 rows + texts).  It lives beside the reference's RocksDict
+        directory ``docs/`` so that saving never writes into a RocksDB database."""
+        return os.path.join(self.folder, "vrq_docs")
 
     def _load_docs(self):
-        p = self._docs_path()
-        if not os.path.exists(os.path.join(p, "int8.npy")):
+        """Rows of the device int8 store in index-row order, from (in this order of preference) this
+        build's ``vrq_docs/`` when it matches ``index.bin``, the reference's RocksDict ``docs/``
+        (``CohereEnhancedVectorDB.py:88``; read by ``docstore.RocksDictReader``, no rocksdict needed), or
+        a round-1 ``docs/int8.npy``.  An index without a matching store is refused: Phases II/III index
+        the int8 rows and norms by index row, so a short store would be read out of bounds."""
+        n = self.index.ntotal
+        own = self._docs_path()
+        legacy = os.path.join(self.folder, "docs")
+        for p in (own, legacy):
+            f = os.path.join(p, "int8.npy")
+            if os.path.exists(f):
+                x8 = np.load(f)
+                if x8.shape[0] == n:
+                    with open(os.path.join(p, "texts.json")) as fh:
+                        self.texts = {int(a): b for a, b in json.load(fh).items()}
+                    self._set_rows(x8)
+                    return
+        if is_rocksdict_dir(legacy):
+            self._load_rocksdict(legacy)
             return
-        x8 = np.load(os.path.join(p, "int8.npy"))
-        if x8.shape[0] != self.index.ntotal:
-            raise RuntimeError("docs/int8.npy does not match index.bin")
-        t = torch.from_numpy(x8).to(self.device)
-        self._x8.append(t)
-        self._norms.append(int8_row_norms(t))
-        with open(os.path.join(p, "texts.json")) as f:
-            self.texts = {int(a): b for a, b in json.load(f).items()}
+        if n:
+            raise DocStoreError(f"{self.folder}: index.bin holds {n} rows but there is no document store "
+                                "(docs/ RocksDict or vrq_docs/) to read their int8 vectors from")
+
+    def _load_rocksdict(self, path):
+        db = RocksDictReader(path)
+        ids = self.index.id_map.cpu().numpy() if isinstance(self.index.id_map, torch.Tensor) else \
+            np.asarray(self.index.id_map)
+        recs = {}
+        for key, val in db.items():
+            try:
+                did = int(key)
+            except (TypeError, ValueError):
+                continue
+            recs[did] = val
+            self.texts[did] = val.get("doc", "N/A") if isinstance(val, dict) else "N/A"
+        x8 = np.zeros((ids.shape[0], self.embedding_dim), np.int8)
+        missing = []
+        for r, did in enumerate(ids.tolist()):
+            v = recs.get(int(did))
+            if not isinstance(v, dict) or "int8" not in v:
+                missing.append(int(did))
+                continue
+            x8[r] = np.asarray(v["int8"], dtype=np.int8).reshape(self.embedding_dim)
+        if missing:
+            # the reference skips such hits in Phase III (:303-305); this build keeps one int8 row per
+            # index row and refuses the inconsistent folder instead
+            raise DocStoreError(f"{path}: no int8 record for index ids {missing[:8]}"
+                                f"{' ...' if len(missing) > 8 else ''}")
+        self._set_rows(x8)
+        logger.info("Loaded %d documents from the RocksDict store %s.", len(recs), path)
+
+    def _set_rows(self, x8: np.ndarray):
+        t = torch.from_numpy(np.ascontiguousarray(x8)).to(self.device)
+        self._x8 = _GrowBuffer((self.embedding_dim,), torch.int8, self.device)
+        self._norms = _GrowBuffer((), torch.float64, self.device)
+        if t.shape[0]:
+            self._x8.append(t)
+            self._norms.append(int8_row_norms(t))
 
     def save(self):
-        """index.bin in FAISS's IBM2 format (:346) + the doc store (int8 rows, texts)."""
+        """index.bin in FAISS's IBM2 format (:346) + this build's doc store (int8 rows, texts) in vrq_docs/."""
         self.index.write(os.path.join(self.folder, "index.bin"))
         p = self._docs_path()
         os.makedirs(p, exist_ok=True)

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from .docstore import DocStoreError, RocksDictReader, is_rocksdict_dir
 from .index import _GrowBuffer, _device, as_device_tensor
 
 logger = logging.getLogger(__name__)
@@ -61,6 +62,9 @@ def flat_ip_topk(xf: torch.Tensor, x8: torch.Tensor, inv_scale: torch.Tensor, bo
     N.check(lib.vrq_flat_ip_topk(N.ptr(xf), N.ptr(x8), N.ptr(inv_scale), N.ptr(bounds), n, qf.shape[1], row_offset,
                                  N.ptr(qf), nq, k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores),
                                  N.ptr(workspace), workspace.numel(), N.stream_handle(dev)), "vrq_flat_ip_topk")
+    if os.environ.get("VRQ_GEMM_FALLBACK") == "0" and bool((cnt < 0).any()):
+        # test hook: the library skipped the exact fallback and left the flagged queries unwritten
+        raise N.VrqNativeError("vrq_flat_ip_topk: queries needed the exact fallback, which VRQ_GEMM_FALLBACK=0 disabled")
     return cnt, rows, scores
 
 
@@ -220,10 +224,30 @@ class CohereVectorDBFloat:
             self.index = FloatIndexIDMap(embedding_dim, device)
         self.device = self.index.device
         self.texts: Dict[int, str] = {}
-        p = os.path.join(folder, "docs", "texts.json")
-        if os.path.exists(p):
-            with open(p) as f:
-                self.texts = {int(a): b for a, b in json.load(f).items()}
+        self._load_texts()
+
+    def _load_texts(self):
+        """Document texts from this build's ``vrq_docs/texts.json`` (or a round-1 ``docs/texts.json``),
+        else from the reference's RocksDict ``docs/`` (``{"doc": text}`` per id, :136; read by
+        ``docstore.RocksDictReader``).  An index without a store is refused: the dedupe of
+        ``add_documents`` (:108-111) and ``remove_document`` (:175) key on the store."""
+        for p in (os.path.join(self.folder, "vrq_docs", "texts.json"), os.path.join(self.folder, "docs", "texts.json")):
+            if os.path.exists(p):
+                with open(p) as f:
+                    self.texts = {int(a): b for a, b in json.load(f).items()}
+                return
+        docs = os.path.join(self.folder, "docs")
+        if is_rocksdict_dir(docs):
+            for key, val in RocksDictReader(docs).items():
+                try:
+                    did = int(key)
+                except (TypeError, ValueError):
+                    continue
+                self.texts[did] = val.get("doc", "N/A") if isinstance(val, dict) else "N/A"
+            return
+        if self.index.ntotal:
+            raise DocStoreError(f"{self.folder}: index.faiss holds {self.index.ntotal} rows but there is no document "
+                                "store (docs/ RocksDict or vrq_docs/texts.json)")
 
     def _setup_config(self, folder: str, model: str, embedding_dim: int):
         config_path = os.path.join(folder, "config.json")
@@ -241,7 +265,7 @@ class CohereVectorDBFloat:
 
     def save(self):
         self.index.write(os.path.join(self.folder, "index.faiss"))
-        p = os.path.join(self.folder, "docs")
+        p = os.path.join(self.folder, "vrq_docs")  # never inside the reference's RocksDB directory
         os.makedirs(p, exist_ok=True)
         with open(os.path.join(p, "texts.json"), "w") as f:
             json.dump({str(a): b for a, b in self.texts.items()}, f)
