@@ -68,6 +68,10 @@ extern "C" {
 #define VRQ_ENC_INT4_LOCAL 4   /* VectorDBInt4._quantize_to_int4 (+min/max) + _to_binary */
 #define VRQ_ENC_BIN_INT16 5    /* VectorDBInt16._to_binary on int16 input */
 #define VRQ_ENC_COHERE 6       /* synthetic Cohere provider: int8 (global limit) + ubinary = packbits(x > 0) */
+/* vrq_rescore_dequant only: the compare_float32 branch of the VectorDB* searches
+ * (VectorDBInt8Global.py:239-240, VectorDBInt8.py:231-232, VectorDBInt4.py:262-263,
+ * VectorDBInt16Global.py:240-241, VectorDBInt4Global.py:257-258): q = f32[n, dim] float rows */
+#define VRQ_RESCORE_F32 16
 
 int vrq_abi_version(void);
 const char* vrq_strerror(int code);
@@ -193,6 +197,7 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
  * ones.  vrq_dequantize writes f32[n, dim]; vrq_rescore_dequant writes, per (query, candidate), the
  * reference score float(np.dot(query_float, dequantised row)) (VectorDBInt8Global.py:232-238 and the
  * same loop in the other classes) as the correctly rounded float32 dot (NaN for negative rows).
+ * vrq_rescore_dequant also takes mode VRQ_RESCORE_F32 (q = the f32 float rows, compare_float32).
  * ------------------------------------------------------------------------- */
 int vrq_dequantize(int32_t mode, const void* q, const double* minmax, int64_t n, int32_t dim, double limit,
                    float* out, void* stream);

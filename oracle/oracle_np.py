@@ -475,3 +475,56 @@ def encode_batch(mode: str, X: np.ndarray, limit: float = 0.3):
     qs = np.stack(qs) if qs else None
     mm = np.array(mm, dtype=np.float64) if mm else None
     return codes, qs, mm
+
+
+# --------------------------------------------------------------------------
+# VectorDBInt{4,8,16}{,Global}: add_documents / remove_document / search
+# --------------------------------------------------------------------------
+class QuantVectorDB:
+    """Restatement of the six VectorDB* classes' document store + search (float vectors in, no HTTP):
+    ``add`` = ``add_documents`` without the embedding call (dedupe by remove, ``add_with_ids`` of the
+    ``_to_binary`` codes, doc store ``{id: (quantised row, min_max, float row)}`` keyed by id, the last
+    write wins -- e.g. ``VectorDBInt8Global.py:162-203``); ``search`` = ``:205-252`` (Phase I
+    top-``min(k * os, ntotal)``, ``float(np.dot(query_float, doc_emb))`` with ``doc_emb`` the
+    dequantised row or the float row (``compare_float32``), stable sort by score desc, first k);
+    ``bin16`` = ``VectorDBInt16.py:221-263`` (Hamming order, score = distance)."""
+
+    def __init__(self, mode: str, limit: float = 0.0, dim: int = 1024):
+        self.mode, self.limit, self.dim = mode, limit, dim
+        self.index = IndexBinaryIDMap2(dim)
+        self.store = {}
+
+    def add(self, ids, X):
+        ids = [int(i) for i in ids]
+        for e in ids:
+            if e in self.store:
+                self.remove(e)
+        codes, q, mm = encode_batch(self.mode, X, self.limit)
+        self.index.add_with_ids(codes, np.asarray(ids, np.int64))
+        for j, e in enumerate(ids):
+            self.store[e] = (None if q is None else q[j], None if mm is None else mm[j], np.asarray(X[j]))
+
+    def remove(self, e):
+        if int(e) in self.store:
+            self.index.remove_ids(np.array([int(e)], np.int64))
+            del self.store[int(e)]
+
+    def search(self, qv, k: int = 10, binary_oversample: int = 10, compare_float32: bool = False):
+        qb, _, _ = encode_batch(self.mode, np.asarray(qv).reshape(1, -1), self.limit)
+        K = min(k * binary_oversample, self.index.ntotal)
+        D, L = self.index.search(qb, K)
+        hits = [(int(e), int(d)) for e, d in zip(L[0], D[0]) if e != -1]
+        if self.mode == "bin16":
+            hits.sort(key=lambda h: h[1])
+            return [(e, float(d)) for e, d in hits[:k]]
+        out = []
+        for e, _ in hits:
+            q, mm, f = self.store[e]
+            if compare_float32:
+                row = np.asarray(f, np.float32).reshape(1, -1)
+            else:
+                row = dequantize(self.mode, q.reshape(1, -1), None if mm is None else mm.reshape(1, 2), self.limit,
+                                 self.dim)
+            out.append((e, float(dequant_scores(np.asarray(qv, np.float32).reshape(1, -1), row)[0, 0])))
+        out.sort(key=lambda h: h[1], reverse=True)
+        return out[:k]

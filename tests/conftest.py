@@ -46,3 +46,15 @@ def oracle_knn(lib, codes, queries, k, threads=0):
                                 D.ctypes.data, I.ctypes.data, threads)
     assert rc == 0
     return D, I
+
+
+@pytest.fixture(scope="session")
+def golden_vdb():
+    import numpy as np
+    return dict(np.load(os.path.join(GOLDEN, "vectordb_synth.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_vdb_real():
+    import numpy as np
+    return dict(np.load(os.path.join(GOLDEN, "vectordb_real.npz")))

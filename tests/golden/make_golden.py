@@ -478,6 +478,177 @@ def gen_flat_real(out_path: str):
     print("wrote", out_path)
 
 
+# ---------------------------------------------------------------------------
+# 4. the six VectorDBInt{4,8,16}{,Global} classes: add_documents + search (+ compare_float32)
+# ---------------------------------------------------------------------------
+VDB_CLASSES = {  # tag -> (module/class, int16 service, folder of the persisted reference data)
+    "int8g": ("VectorDBInt8Global", False, "db_int8_global"),
+    "int16g": ("VectorDBInt16Global", False, "db_int16_global"),
+    "int4g": ("VectorDBInt4Global", False, "db_int4_global"),
+    "int8": ("VectorDBInt8", False, "db_int8"),
+    "int4": ("VectorDBInt4", False, "db_int4"),
+    "bin16": ("VectorDBInt16", True, "db_int16"),
+}
+VDB_SEARCHES = {"k10": (10, 10), "k5": (5, 3), "k30": (30, 2)}
+
+
+class _Resp:
+    def __init__(self, d):
+        self._d = d
+
+    def raise_for_status(self):
+        pass
+
+    def json(self):
+        return self._d
+
+
+class _FakeRequests:
+    """Stands in for ``requests`` inside a reference VectorDB* module: the embedding service is a
+    table lookup ({text: vector}); an unknown text fails like an HTTP error."""
+
+    def __init__(self, table):
+        self.table = table
+
+    def post(self, url, json=None, **kw):
+        if "texts" in json:        # VectorDBInt16._generate_int16_embeddings (:116-128)
+            return _Resp({"embeddings": [self.table[t].tolist() for t in json["texts"]]})
+        t = json["input"]          # VectorDBInt*._generate_embeddings (e.g. VectorDBInt8Global.py:96-103)
+        if t not in self.table:
+            raise RuntimeError(f"no embedding for {t!r}")
+        return _Resp({"embeddings": [self.table[t].tolist()]})
+
+
+class _Int4AsPyInts(dict):
+    """Doc store for the int4 classes: ``get`` hands the packed int4 bytes to the reference's
+    ``_dequantize_int4`` as Python ints, which runs the unmodified nibble loop with its NumPy-1
+    result (under NumPy 2 ``byte + 256`` on np.int8 raises OverflowError)."""
+
+    def get(self, key, default=None):
+        v = dict.get(self, key, default)
+        if isinstance(v, dict) and "emb_int4" in v:
+            v = dict(v, emb_int4=[int(b) for b in np.asarray(v["emb_int4"]).reshape(-1)])
+        return v
+
+
+def _ref_vdb(tag, table, folder="/nonexistent", config=None):
+    name, i16, _ = VDB_CLASSES[tag]
+    mod = _import_ref(name)
+    mod.requests = _FakeRequests(table)
+    cls = getattr(mod, name)
+    db = object.__new__(cls)           # skip __init__ (Rdict / folders)
+    db.embedding_dim = 1024
+    db.model = "snowflake-arctic-embed2"
+    db.embed_url = "http://embed.invalid/api/embed"
+    db.folder = folder
+    db.config = dict(config or {"version": "1.0", "model": db.model, "embedding_dim": 1024})
+    if tag in ("int8g", "int16g", "int4g"):
+        db.global_limit = float(db.config.setdefault("global_limit", {"int8g": 0.3, "int16g": 1.0, "int4g": 0.18}[tag]))
+    db.index = O.IndexBinaryIDMap2(1024)
+    db.doc_db = _Int4AsPyInts() if tag in ("int4", "int4g") else {}
+    if not i16:
+        db.float_embeddings = {}
+    db.save = lambda: None
+    return db
+
+
+def _vdb_searches(db, tag, queries, table, out, prefix, flags=(False, True)):
+    for cname, (k, osb) in VDB_SEARCHES.items():
+        for cf in (flags if tag != "bin16" else (False,)):
+            nq = queries.shape[0]
+            ids = np.full((nq, k), -1, np.int64)
+            sc = np.full((nq, k), np.nan)
+            cnt = np.zeros(nq, np.int64)
+            err = np.zeros(nq, np.int64)
+            for j in range(nq):
+                qt = f"{prefix}q{j}"
+                table[qt] = queries[j]
+                try:
+                    r = db.search(qt, k=k, binary_oversample=osb) if tag == "bin16" else \
+                        db.search(qt, k=k, binary_oversample=osb, compare_float32=cf)
+                except KeyError:
+                    err[j] = 1
+                    continue
+                cnt[j] = len(r)
+                for i, h in enumerate(r):
+                    ids[j, i] = h["doc_id"]
+                    sc[j, i] = h["score"]
+            key = f"{prefix}{tag}_{cname}_{'f32' if cf else 'q'}"
+            out.update({f"{key}_ids": ids, f"{key}_score": sc, f"{key}_cnt": cnt, f"{key}_keyerror": err})
+
+
+def gen_vectordb_synth(out_path: str):
+    """Every VectorDB* class's own ``add_documents`` / ``remove_document`` / ``search`` (both
+    ``compare_float32`` values) on a synthetic clustered corpus, the embedding service a table:
+    700 docs in 64-doc batches (planted duplicate vectors), two removals, a re-add under a new text,
+    and one id added twice in one call (the doc store keeps the last; both rows stay in the index)."""
+    rng = np.random.default_rng(4242)
+    N = 700
+    F = synth_corpus(rng, N, nclusters=24)
+    for a, b in ((3, 400), (4, 401), (4, 402)):
+        F[b] = F[a]
+    X16 = np.clip(np.round(F * 40000.0), -32767, 32767).astype(np.int16)
+    texts = [f"t{i}" for i in range(N)]
+    ids = (np.arange(N, dtype=np.int64) * 2 + 100).tolist()
+    nq = 20
+    src = rng.integers(0, N, nq)
+    src[0], src[1] = 3, 4
+    QF = (F[src] + (0.4 / 32.0) * rng.standard_normal((nq, 1024))).astype(np.float32)
+    QF[0] = F[3]
+    Q16 = np.clip(np.round(QF * 40000.0), -32767, 32767).astype(np.int16)
+    res = {"F": F, "X16": X16, "ids": np.array(ids), "QF": QF, "Q16": Q16}
+    for tag in VDB_CLASSES:
+        i16 = VDB_CLASSES[tag][1]
+        table = {t: (X16[i] if i16 else F[i]) for i, t in enumerate(texts)}
+        db = _ref_vdb(tag, table)
+        db.add_documents(ids, texts, batch_size=64, save=False)
+        db.remove_document(ids[10], save=False)
+        db.remove_document(ids[11], save=False)
+        db.add_documents([ids[11], 9001, 9001], ["t12", "t5", "t6"], save=False)
+        res[f"{tag}_id_map"] = db.index.id_map.copy()
+        res[f"{tag}_codes"] = db.index.xb.copy()
+        _vdb_searches(db, tag, Q16 if i16 else QF, table, res, "")
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
+
+
+def gen_vectordb_real(out_path: str):
+    """The same classes' ``search`` on the reference's persisted 1000-document folders
+    (``db_int8_global`` ... ``db_int16``: index.bin + the RocksDict SST), opened the way the
+    reference's constructor opens them (``faiss.read_index_binary`` + ``Rdict``).  The SST values are
+    read by the product's ``docstore.RocksDictReader`` (a restricted pickle interpreter that executes
+    nothing; cross-checked against this script's own SST walker in tests/test_docstore.py).  No float
+    embeddings are persisted, so the reference's ``compare_float32=True`` search raises KeyError on
+    these folders (recorded as ``keyerror``); the float queries are dequantised db_int8_global rows
+    plus noise, the int16 ones db_int16's stored int16 rows plus noise."""
+    from vectorragquantization_amd.docstore import RocksDictReader
+    rng = np.random.default_rng(77)
+    base = RocksDictReader(os.path.join(REF, "db_int8_global/docs"))
+    X8 = np.stack([np.asarray(base[str(i)]["emb_int8"], np.int8) for i in range(1000)])
+    s16 = RocksDictReader(os.path.join(REF, "db_int16/docs"))
+    X16 = np.stack([np.asarray(s16[str(i)]["emb_int16"], np.int16) for i in range(1000)])
+    nq = 24
+    src = rng.integers(0, 1000, nq)
+    QF = (X8[src].astype(np.float32) * np.float32(0.3 / 127) +
+          (0.2 / 32.0) * rng.standard_normal((nq, 1024))).astype(np.float32)
+    Q16 = np.clip(X16[src].astype(np.int64) + rng.integers(-200, 200, (nq, 1024)), -32767, 32767).astype(np.int16)
+    res = {"QF": QF, "Q16": Q16}
+    for tag, (name, i16, folder) in VDB_CLASSES.items():
+        import json as _json
+        cfg = _json.load(open(os.path.join(REF, folder, "config.json")))
+        table = {}
+        db = _ref_vdb(tag, table, os.path.join(REF, folder), cfg)
+        xb, idm = read_ibm2(os.path.join(REF, folder, "index.bin"))
+        db.index.add_with_ids(xb, idm)
+        store = RocksDictReader(os.path.join(REF, folder, "docs"))
+        for key, val in store.items():
+            dict.__setitem__(db.doc_db, key, val)
+        res[f"{tag}_ntotal"] = np.int64(db.index.ntotal)
+        _vdb_searches(db, tag, Q16 if i16 else QF, table, res, "", flags=(False, True))
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
+
+
 def gen_ref_db(out_dir: str):
     """Byte copies of persisted reference data files (no source): the folders tests open."""
     import shutil
@@ -485,6 +656,8 @@ def gen_ref_db(out_dir: str):
              "db_cohere_enhanced/docs/CURRENT", "db_cohere_float/config.json", "db_cohere_float/docs/000009.sst",
              "db_cohere_float/docs/CURRENT", "db_int4_global/config.json", "db_int4_global/index.bin",
              "db_int4_global/docs/000009.sst", "db_int4_global/docs/CURRENT"]
+    for folder in ("db_int8_global", "db_int16_global", "db_int8", "db_int4", "db_int16"):
+        files += [f"{folder}/config.json", f"{folder}/index.bin", f"{folder}/docs/000009.sst", f"{folder}/docs/CURRENT"]
     for f in files:
         dst = os.path.join(out_dir, f)
         os.makedirs(os.path.dirname(dst), exist_ok=True)
@@ -507,5 +680,9 @@ if __name__ == "__main__":
         gen_search_real(os.path.join(HERE, "search_real.npz"))
     if not only or "flat_real" in only:
         gen_flat_real(os.path.join(HERE, "flat_real.npz"))
+    if not only or "vectordb_synth" in only:
+        gen_vectordb_synth(os.path.join(HERE, "vectordb_synth.npz"))
+    if not only or "vectordb_real" in only:
+        gen_vectordb_real(os.path.join(HERE, "vectordb_real.npz"))
     if not only or "ref_db" in only:
         gen_ref_db(os.path.join(HERE, "ref_db"))

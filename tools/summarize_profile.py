@@ -51,11 +51,11 @@ def pmc(path):
 
 def main(src, dst, tag):
     out = {"tag": tag, "source": src}
-    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         out["kernel_stats"] = [r for r in csv.DictReader(open(stats[0]))]
     for name in ("pmc_sq", "pmc_mfma", "pmc_v", "pmc_fetch", "pmc_write"):
-        f = glob.glob(os.path.join(src, name, "*counter_collection.csv"))
+        f = glob.glob(os.path.join(src, name, "**", "*counter_collection.csv"), recursive=True)
         if f:
             out[name] = pmc(f[0])
     # per-launch HBM bytes of every kernel seen by both traffic passes

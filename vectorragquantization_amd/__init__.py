@@ -8,7 +8,11 @@ quantise/packbits encode path, as hand-written HIP kernels behind a C ABI
 from ._native import VrqNativeError, load as load_native  # noqa: F401
 
 __all__ = ["VrqNativeError", "load_native", "CohereEnhancedVectorDB", "BinaryIndexIDMap2", "encode",
-           "ShardedSearch"]
+           "ShardedSearch", "CohereVectorDBFloat", "VectorDBInt8Global", "VectorDBInt16Global", "VectorDBInt4Global",
+           "VectorDBInt8", "VectorDBInt4", "VectorDBInt16"]
+
+_VECTORDB = ("VectorDBInt8Global", "VectorDBInt16Global", "VectorDBInt4Global", "VectorDBInt8", "VectorDBInt4",
+             "VectorDBInt16")
 
 
 def __getattr__(name):  # lazy: importing the package must not require a GPU
@@ -21,6 +25,12 @@ def __getattr__(name):  # lazy: importing the package must not require a GPU
     if name == "encode":
         from .quant import encode
         return encode
+    if name in _VECTORDB:
+        from . import vectordb
+        return getattr(vectordb, name)
+    if name == "CohereVectorDBFloat":
+        from .flat import CohereVectorDBFloat
+        return CohereVectorDBFloat
     if name == "ShardedSearch":
         from .dist import ShardedSearch
         return ShardedSearch

@@ -32,6 +32,7 @@ VRQ_GEMM_FLOAT_IP = 4
 VRQ_GEMM_STAGE_SAMPLE = 16
 VRQ_GEMM_STAGE_MAIN = 32
 VRQ_GEMM_STAGE_FINISH = 64
+VRQ_RESCORE_F32 = 16  # vrq_rescore_dequant: compare_float32 rows
 VRQ_SCAN_KIND_VALU = 0
 VRQ_SCAN_KIND_MFMA = 1
 

@@ -13,6 +13,8 @@
 // Rescoring (VectorDBInt8Global.py:232-238 and the same loop in the other classes):
 //   score = float(np.dot(query_float, dequantised row)), a float32 dot: computed here as the exact
 //   f64 sum of the exact f32 x f32 products rounded once to f32 (NumPy's sdot is within a few ulp).
+//   VRQ_RESCORE_F32 (rescoring only): the compare_float32 branch (VectorDBInt8Global.py:239-240 and
+//   the same branch in the other classes) -- q is the f32 float_embeddings rows, used as they are.
 #include "vrq_internal.h"
 
 namespace vrq {
@@ -30,6 +32,7 @@ struct DeqRow {
 __device__ __forceinline__ DeqRow deq_row(int mode, double limit, const double* minmax, int64_t r) {
   DeqRow d{mode, limit, 0.f, 0.0, false};
   switch (mode) {
+    case VRQ_RESCORE_F32: break;
     case VRQ_ENC_INT8_GLOBAL: d.sf = (float)(limit / 127.0); break;
     case VRQ_ENC_INT16_GLOBAL: d.sf = (float)(limit / 32767.0); break;
     case VRQ_ENC_INT4_GLOBAL: d.sd = limit / 7.0; break;
@@ -53,6 +56,8 @@ __device__ __forceinline__ DeqRow deq_row(int mode, double limit, const double* 
 __device__ __forceinline__ float deq_elem(const DeqRow& d, const void* q, int64_t r, int dim, int i) {
   if (d.zero) return 0.f;
   switch (d.mode) {
+    case VRQ_RESCORE_F32:
+      return reinterpret_cast<const float*>(q)[r * dim + i];
     case VRQ_ENC_INT8_GLOBAL:
     case VRQ_ENC_INT8_LOCAL:
       return __fmul_rn((float)reinterpret_cast<const int8_t*>(q)[r * dim + i], d.sf);
@@ -129,7 +134,7 @@ int vrq_dequantize(int32_t mode, const void* q, const double* minmax, int64_t n,
 int vrq_rescore_dequant(int32_t mode, const float* qf, int32_t nq, int32_t dim, const void* q, const double* minmax,
                         double limit, int64_t n, const int64_t* cand_rows, int32_t ncand, double* out,
                         void* stream) {
-  VRQ_CHECK_ARG(mode >= VRQ_ENC_INT8_GLOBAL && mode <= VRQ_ENC_INT4_LOCAL);
+  VRQ_CHECK_ARG((mode >= VRQ_ENC_INT8_GLOBAL && mode <= VRQ_ENC_INT4_LOCAL) || mode == VRQ_RESCORE_F32);
   VRQ_CHECK_ARG(nq >= 0 && ncand >= 0 && n >= 0 && dim > 0);
   if (dim > DQ_MAX_DIM) return VRQ_EUNSUPPORTED;
   if (nq == 0 || ncand == 0) return VRQ_OK;

@@ -1,5 +1,16 @@
 """Embedding providers (the reference's L1 layer) -- plumbing, not the hot path.
 
+``OllamaHTTPProvider`` reproduces the ``VectorDBInt{4,8}{,Global}`` /
+``VectorDBInt16Global`` ``_generate_embeddings`` request (e.g.
+``VectorDBInt8Global.py:88-128``): one POST per text of ``{"model", "input"}`` to
+``embed_url`` (default ``http://localhost:11434/api/embed``), the vector taken
+from ``data[0].embedding`` or ``embeddings`` (squeezed), texts whose vector is
+missing or of the wrong dimension skipped with a log line.  ``Int16HTTPProvider``
+is ``VectorDBInt16._generate_int16_embeddings`` (``VectorDBInt16.py:92-146``):
+one POST of ``{"model", "texts", "embedding_bits": 16}`` for the whole batch.
+Both return ``{text: vector}`` like the reference; quantisation happens on the
+GPU for the whole batch (``vrq_encode``).
+
 ``CohereHTTPProvider`` reproduces ``CohereEnhancedVectorDB._get_embeddings``
 (``CohereEnhancedVectorDB.py:136-169``): one JSON POST to ``/v2/embed`` with
 ``model``, ``texts``, ``input_type``, ``truncate: NONE``, ``embedding_types``;
@@ -47,6 +58,81 @@ class CohereHTTPProvider:
         except Exception as e:  # same contract as the reference: log + {}
             logger.error("Embedding generation failed: %s", str(e))
             return {}
+
+
+class OllamaHTTPProvider:
+    def __init__(self, embed_url: str = "http://localhost:11434/api/embed", model: str = "snowflake-arctic-embed2",
+                 embedding_dim: int = 1024):
+        self.embed_url, self.model, self.dim = embed_url, model, embedding_dim
+
+    def embed_floats(self, texts) -> dict:
+        import requests
+        out = {}
+        for text in texts:
+            try:
+                r = requests.post(self.embed_url, json={"model": self.model, "input": text})
+                r.raise_for_status()
+                data = r.json()
+                if "data" in data and data["data"]:
+                    e = np.array(data["data"][0]["embedding"], dtype=np.float32)
+                elif "embeddings" in data and data["embeddings"]:
+                    e = np.array(data["embeddings"], dtype=np.float32)
+                else:
+                    logger.warning(f"No embedding generated for text: {text}")
+                    continue
+                if e.ndim > 1:
+                    e = e[0]
+                if e.shape[0] != self.dim:
+                    logger.error(f"Unexpected embedding dimension: {e.shape[0]}. Expected: {self.dim}. "
+                                 f"Skipping '{text}'.")
+                    continue
+                out[text] = e
+            except Exception as ex:  # the reference logs and skips the text
+                logger.error(f"Failed to generate embedding for text: '{text}'. Error: {ex}")
+        return out
+
+
+class Int16HTTPProvider:
+    def __init__(self, embed_url: str = "http://localhost:11434/api/embed", model: str = "snowflake-arctic-embed2",
+                 embedding_dim: int = 1024):
+        self.embed_url, self.model, self.dim = embed_url, model, embedding_dim
+
+    def embed_int16(self, texts) -> dict:
+        import requests
+        out = {}
+        if not texts:
+            return out
+        try:
+            r = requests.post(self.embed_url, json={"model": self.model, "texts": list(texts), "embedding_bits": 16})
+            r.raise_for_status()
+        except Exception as ex:
+            logger.error(f"Int16 embedding generation failed: {ex}")
+            return out
+        emb = r.json().get("embeddings", [])
+        if len(emb) != len(texts):
+            logger.error(f"Mismatch: got {len(emb)} embeddings for {len(texts)} texts.")
+            return out
+        for i, text in enumerate(texts):
+            a = np.array(emb[i], dtype=np.int16)
+            if a.shape[0] != self.dim:
+                logger.error(f"Dimension mismatch for text={text}. Got {a.shape[0]}, expected {self.dim}")
+                continue
+            out[text] = a
+        return out
+
+
+class TableProvider:
+    """Offline provider for tests and benchmarks: ``{text: vector}`` lookups (float32 or int16
+    vectors), texts not in the table skipped like a failed request."""
+
+    def __init__(self, table: dict):
+        self.table = table
+
+    def embed_floats(self, texts) -> dict:
+        return {t: np.asarray(self.table[t], dtype=np.float32) for t in texts if t in self.table}
+
+    def embed_int16(self, texts) -> dict:
+        return {t: np.asarray(self.table[t], dtype=np.int16) for t in texts if t in self.table}
 
 
 def text_seed(text: str) -> int:

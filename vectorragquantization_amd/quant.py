@@ -84,13 +84,18 @@ def dequantize(mode: str, q, minmax=None, limit: float = 0.0, dim: int = None, d
 
 
 def vectordb_search(mode: str, codes: torch.Tensor, q: torch.Tensor, qf: torch.Tensor, qb: torch.Tensor, k: int = 10,
-                    binary_oversample: int = 10, minmax: torch.Tensor = None, limit: float = 0.0):
-    """``VectorDBInt{4,8,16}{,Global}.search`` for a query batch (e.g. VectorDBInt8Global.py:205-243):
+                    binary_oversample: int = 10, minmax: torch.Tensor = None, limit: float = 0.0,
+                    rescore_row: torch.Tensor = None):
+    """``VectorDBInt{4,8,16}{,Global}.search`` for a query batch (e.g. VectorDBInt8Global.py:205-252):
     Phase I Hamming top-``k * binary_oversample`` over the ubinary codes (``vrq_hamming_topk``, FAISS
-    order), Phase II ``float(np.dot(query_float, dequantised row))`` (``vrq_rescore_dequant``), stable
-    sort by score descending, first k.  ``mode="bin16"`` (VectorDBInt16.search) stops after Phase I
-    and ranks by Hamming distance.  Returns (rows i64[nq, k], hamming i32[nq, k], score f64[nq, k])
-    on the device; rows past the corpus are -1 (score NaN)."""
+    order), Phase II ``float(np.dot(query_float, doc_emb))`` (``vrq_rescore_dequant``), Python's stable
+    sort by score descending, first k.  ``doc_emb`` is the dequantised row of ``mode`` or, for
+    ``mode="f32"`` (the ``compare_float32`` branch, ``:239-240``), the f32 float row ``q``.
+    ``mode="bin16"`` (VectorDBInt16.search) stops after Phase I and ranks by Hamming distance.
+    ``rescore_row`` (i64[n], optional) maps an index row to the row whose stored vector the
+    reference's ``doc_db[str(id)]`` lookup returns (the last add of a duplicated id).
+    Returns (rows i64[nq, k], hamming i32[nq, k], score f64[nq, k]) on the device; rows past the
+    corpus are -1 (score NaN)."""
     dev = codes.device
     n, cb = codes.shape
     nq = qb.shape[0]
@@ -105,12 +110,19 @@ def vectordb_search(mode: str, codes: torch.Tensor, q: torch.Tensor, qf: torch.T
     if mode == "bin16":
         kk = min(k, K)
         return rows[:, :kk], dist[:, :kk], dist[:, :kk].to(torch.float64)
+    if q is None or q.shape[0] != n or (minmax is not None and minmax.shape[0] != n):
+        # the ABI indexes q / minmax by candidate row and cannot see their lengths
+        raise N.VrqNativeError(f"vectordb_search: {n} code rows but {None if q is None else q.shape[0]} stored rows")
+    cand = rows
+    if rescore_row is not None:
+        cand = torch.where(rows >= 0, rescore_row[rows.clamp_min(0)], rows).contiguous()
     score = torch.empty((nq, K), dtype=torch.float64, device=dev)
     d = qf.shape[1]
+    m = N.VRQ_RESCORE_F32 if mode == "f32" else _DEQ_MODES[mode]
     with torch.cuda.device(dev):
-        N.check(lib.vrq_rescore_dequant(_DEQ_MODES[mode], N.ptr(qf), nq, d, N.ptr(q), N.ptr(minmax), float(limit), n,
-                                        N.ptr(rows), K, N.ptr(score), N.stream_handle(dev)), "vrq_rescore_dequant")
-    # Python's stable sort by score desc over the Phase-I order (VectorDBInt8Global.py:241);
+        N.check(lib.vrq_rescore_dequant(m, N.ptr(qf), nq, d, N.ptr(q), N.ptr(minmax), float(limit), n,
+                                        N.ptr(cand), K, N.ptr(score), N.stream_handle(dev)), "vrq_rescore_dequant")
+    # Python's stable sort by score desc over the Phase-I order (VectorDBInt8Global.py:251);
     # missing candidates (-1) sort last, -0.0 ties +0.0
     key = torch.where(rows >= 0, score + 0.0, torch.full_like(score, float("-inf")))
     o = torch.sort(-key, dim=1, stable=True).indices[:, :k]
