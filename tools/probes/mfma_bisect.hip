@@ -39,9 +39,14 @@ int main(int argc, char** argv) {
   float best = 1e30f;
   for (int it = 0; it < 6; ++it) {
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(vrq::hamming_mfma_kernel<vrq::MFMA_MAIN>, dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0, 0, codes,
-                       n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
-                       (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
+    if (p.mb == 4)
+      hipLaunchKernelGGL((vrq::hamming_mfma_kernel<vrq::MFMA_MAIN, 4>), dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0,
+                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks,
+                         p.nqb, (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
+    else
+      hipLaunchKernelGGL((vrq::hamming_mfma_kernel<vrq::MFMA_MAIN, 2>), dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0,
+                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks,
+                         p.nqb, (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -51,9 +56,9 @@ int main(int argc, char** argv) {
   const double rows = (double)n;
   const double tiles_per_wg = (double)p.chunk_rows / vrq::RT;
   const double ops = rows * nq * 2048.0;
-  printf("{\"bisect\": %d, \"n\": %lld, \"nq\": %d, \"ms\": %.4f, \"us_per_tile\": %.3f, \"TOPS\": %.1f, "
+  printf("{\"mb\": %d, \"bisect\": %d, \"n\": %lld, \"nq\": %d, \"ms\": %.4f, \"us_per_tile\": %.3f, \"TOPS\": %.1f, "
          "\"mfma_frac_fp4_dense_10066\": %.3f}\n",
-         VRQ_BISECT, (long long)n, nq, best, best * 1e3 / tiles_per_wg, ops / (best * 1e-3) / 1e12,
+         p.mb, VRQ_BISECT, (long long)n, nq, best, best * 1e3 / tiles_per_wg, ops / (best * 1e-3) / 1e12,
          ops / (best * 1e-3) / 1e12 / 10066.0);
   return 0;
 }

@@ -43,15 +43,15 @@
 
 namespace vrq {
 
-
 constexpr int MWAVES = 4;                   // waves per workgroup (one per SIMD)
-constexpr int QPW = 64;                     // queries per wave (2 M-blocks of 32)
-constexpr int QPB = MWAVES * QPW;           // queries per workgroup (256)
 constexpr int RT = 64;                      // rows per tile (2 n-blocks of 32)
 constexpr int KS = 16;                      // k-steps of 64 bits (1024-bit codes)
 constexpr int NG = 2 * KS;                  // k-step groups per tile (n-block, k-step)
 constexpr int PKT = RT * 128;               // packed tile bytes (8 KiB)
-constexpr int NPK = 4;                      // packed ring depth (DMA issued 4 tiles ahead)
+#ifndef VRQ_NPK
+#define VRQ_NPK 4
+#endif
+constexpr int NPK = VRQ_NPK;                // packed ring depth (DMA issued NPK tiles ahead)
 constexpr int NUB = 3;                      // unpacked ring: tile t read, t+1 ready, t+2 written
 constexpr int UBT = NG * 1024;              // unpacked tile bytes (32 KiB)
 constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per tile (2)
@@ -66,52 +66,73 @@ constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per
 constexpr int BAHEAD = VRQ_BAHEAD;          // B fragments read this many groups ahead
 constexpr int NRING = BAHEAD < 4 ? 4 : 8;   // B fragment ring (power of two > BAHEAD)
 constexpr int STG = 512;                    // per-wave staged hit entries (u32)
-constexpr int SMEM_BYTES = NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * QPW * 4 + MWAVES * (STG + 1) * 4;
-constexpr int E8M0_TWO = 128;               // MX block scale 2^1
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
-static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
+// M-blocks (32 queries each) per wave: MB = 4 for large batches (512 queries per workgroup, each
+// B fragment feeds 4 MFMAs), MB = 2 below (256 per workgroup)
+template <int MB>
+struct MfmaShape {
+  static constexpr int QPW = 32 * MB;                 // queries per wave
+  static constexpr int QPB = MWAVES * QPW;            // queries per workgroup
+  static constexpr int SMEM =
+      NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * QPW * 8 + MWAVES * (STG + 1) * 4 + MWAVES * MB * 128;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
+constexpr int kMbLarge = 4, kMbSmall = 2;
+constexpr int kMbLargeMinQueries = 512;     // batches of >= 512 queries take the MB = 4 kernel
 
-// 32 code bits -> one FP4 MFMA fragment lane: 32 e2m1 values, code 0x1 (0.5) per set bit.
-// Dword j, nibble i holds bit 4i + j: a fixed permutation of k applied identically to queries
-// (A) and rows (B), so every dot product is unchanged.
-__device__ __forceinline__ v4i unpack32(uint32_t bits) {
+// 32 code bits -> one FP4 MFMA fragment lane: 32 e2m1 values.  Dword j, nibble i holds bit 4i + j
+// (a fixed permutation of k applied identically to queries and rows, so every dot product is
+// unchanged), encoded so that A x B = 1 per common set bit:
+//   rows (B):    j = 0, 1, 2: w & (0x11111111 << j) -> codes 0x1 / 0x2 / 0x4 = 0.5 / 1 / 2;
+//                j = 3: (w >> 1) & 0x44444444 -> 0x4 = 2           (5 VALU per 32 bits)
+//   queries (A): 2 / 1 / 0.5 / 0.5 at the same positions (unpacked once per kernel)
+__device__ __forceinline__ v4i unpack_row32(uint32_t w) {
   v4i r;
-  r.x = (int)(bits & 0x11111111u);
-  r.y = (int)((bits >> 1) & 0x11111111u);
-  r.z = (int)((bits >> 2) & 0x11111111u);
-  r.w = (int)((bits >> 3) & 0x11111111u);
+  r.x = (int)(w & 0x11111111u);
+  r.y = (int)(w & 0x22222222u);
+  r.z = (int)(w & 0x44444444u);
+  r.w = (int)((w >> 1) & 0x44444444u);
+  return r;
+}
+__device__ __forceinline__ v4i unpack_query32(uint32_t w) {
+  v4i r;
+  r.x = (int)((w << 2) & 0x44444444u);
+  r.y = (int)(w & 0x22222222u);
+  r.z = (int)((w >> 2) & 0x11111111u);
+  r.w = (int)((w >> 3) & 0x11111111u);
   return r;
 }
 
-// (0.5 * 2^1) * (0.5 * 2^1) = 1 per common set bit: C + popcount(q & r) exactly (<= 1024 in f32).
+// Unscaled v_mfma_f32_32x32x64_f8f6f4 (scale operands 0 select the unscaled form, 32 cycles; the
+// block-scaled form costs 33 on these operands, tools/probes/mfma_shape_probe.hip): 1 per common
+// set bit (unpack_row32 x unpack_query32), so C + popcount(q & r) exactly (integers <= 1024 in f32).
 // FP4 operands occupy 4 registers; the upper half of the 8-register operand is ignored.
 __device__ __forceinline__ v16f mfma_fp4(const v4i& a, const v4i& b, const v16f& c) {
   const v8i a8 = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
   const v8i b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, FMT_FP4, FMT_FP4, 0, E8M0_TWO, 0, E8M0_TWO);
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, FMT_FP4, FMT_FP4, 0, 0, 0, 0);
 }
 
 
 // Packed tile image: 16-byte piece c of tile row r lives at slot r*8 + (c ^ ((r>>1)&7)).
 __device__ __forceinline__ int pk_slot(int r, int c) { return r * 8 + (c ^ ((r >> 1) & 7)); }
 
-// wave-uniform "any lane has a value > thr in these 16 registers"
+// wave-uniform "any lane has a value > thr in these 16 registers", for thr >= 0: a signed-integer
+// max3 tree over the float bit patterns (non-negative floats order like their bits; negative ones
+// are below every non-negative pattern, and none of them can exceed thr >= 0), no canonicalisation
 __device__ __forceinline__ bool any_above(const v16f& a, float thr) {
-  float mx = fmaxf(fmaxf(a[0], a[1]), a[2]);
-  mx = fmaxf(fmaxf(mx, a[3]), a[4]);
-  mx = fmaxf(fmaxf(mx, a[5]), a[6]);
-  mx = fmaxf(fmaxf(mx, a[7]), a[8]);
-  mx = fmaxf(fmaxf(mx, a[9]), a[10]);
-  mx = fmaxf(fmaxf(mx, a[11]), a[12]);
-  mx = fmaxf(fmaxf(mx, a[13]), a[14]);
-  mx = fmaxf(mx, a[15]);
-  return __ballot(mx > thr) != 0;
+  const v16i b = __builtin_bit_cast(v16i, a);
+  // tree of depth 3: five independent max3, then two, then one
+  const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
+  const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
+  const int y0 = max(max(x0, x1), x2), y1 = max(max(x3, x4), b[15]);
+  return __ballot(max(y0, y1) > __float_as_int(thr)) != 0;
 }
 
-// Staged hit entry (u32): (v + 1024) << 13 | query-in-wave << 7 | row - (t-1)*64, where
+// Staged hit entry (u32): (v + 1024) << 14 | query-in-wave << 7 | row - (t-1)*64, where
 // v = dist - pc(q) in [-1024, 1024] and the row is relative to the previous tile's first row
 // (the epilogue of a tile's second n-block runs in the next tile's iteration).
-constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
+constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7;
 
 // DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) is written
 // as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + row].  Chunk c covers
@@ -120,21 +141,32 @@ constexpr int ENT_V_SHIFT = 13, ENT_Q_SHIFT = 7;
 // MODE: MFMA_MAIN (thresholded pass), MFMA_SAMPLE (dense sample pass, DENSE below) or MFMA_RERUN
 // (the exact re-run of failed query blocks: same code as MAIN, a separate symbol so profiles and
 // traces tell the two launches apart).
+//
+// Schedule of the 32 k-step groups of a tile (group gi = (n-block gi>>4, k-step j = gi&15)): every
+// group reads the B fragment of group gi+BAHEAD (one ds_read_b128, immediate offset) and runs MB
+// MFMAs on the fragment of group gi.  Around them, spread so no group's vector work much exceeds
+// its MFMA shadow: the packed reads of unpack unit u (gi = 8u+1) and its unpack + LDS writes
+// (gi = 8u+6), the row-popcount reads (gi = 12) and writes (gi = 28); for the previous n-block the
+// hit test of M-block m (j = 2+m), one branch to the (rare) hit extraction (j = 3+MB) and the
+// accumulator re-seeds (j = 4+MB, two M-blocks per group); the asynchronous hit flush
+// (gi = 20+MB and 24+MB).
 enum { MFMA_MAIN = 0, MFMA_SAMPLE = 1, MFMA_RERUN = 2 };
-template <int MODE>
+template <int MODE, int MB>
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM_BYTES];
+  constexpr int QPW = MfmaShape<MB>::QPW, QPB = MfmaShape<MB>::QPB;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[MfmaShape<MB>::SMEM];
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
   int32_t* pcr = (int32_t*)(smem + NPK * PKT + NUB * UBT);  // NUB x 64 row popcounts
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int32_t* lcnt = pcr + NUB * RT + w * QPW;                 // this wave's 64 list lengths
-  int32_t* stg = pcr + NUB * RT + MWAVES * QPW + w * (STG + 1);  // this wave's hit staging (+1 spare)
+  int32_t* lcnt = pcr + NUB * RT + w * QPW;                 // this wave's list lengths
+  int32_t* tq = pcr + NUB * RT + MWAVES * QPW + w * QPW;    // this wave's tau'(q) = tau(q) - pc(q)
+  int32_t* stg = pcr + NUB * RT + 2 * MWAVES * QPW + w * (STG + 1);  // this wave's hit staging (+1 spare)
 
   const int l = lane_id();
   const int h = l >> 5, ri = l & 31;
@@ -153,42 +185,57 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   const int nrows = (int)(row1 - row0);
   const int ntiles = (nrows + RT - 1) / RT;
 
-  auto issue = [&](int t) {
+  // LDS-DMA of packed tile t: this wave's GPW pieces of 64 x 16 B (lane -> (row, piece) through the
+  // swizzle).  Whole tiles take a uniform base + a fixed per-lane offset; the last partial tile
+  // clamps each row to the chunk's last row.
+  uint32_t doff[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    const int p = (w * GPW + i) * 64 + l;
+    const int r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
+    doff[i] = (uint32_t)(r * 128 + c * 16);
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
     uint8_t* buf = pk + (t % NPK) * PKT;
     const int64_t tr0 = row0 + (int64_t)t * RT;
+    if (tr0 + RT <= row1) {
+      const uint8_t* base = codes + tr0 * 128;
 #pragma unroll
-    for (int i = 0; i < GPW; ++i) {
-      const int gi = w * GPW + i;
-      const int p = gi * 64 + l;  // LDS slot written by this lane
-      const int r = p >> 3, cs = p & 7;
-      const int c = cs ^ ((r >> 1) & 7);
-      int64_t row = tr0 + r;
-      row = row < row1 ? row : row1 - 1;
-      __builtin_amdgcn_global_load_lds(codes + row * 128 + c * 16,
-                                       (__attribute__((address_space(3))) void*)(buf + gi * 1024), 16, 0, 0);
+      for (int i = 0; i < GPW; ++i)
+        __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + (w * GPW + i) * 1024),
+                                         16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        int64_t row = tr0 + (doff[i] >> 7);
+        row = row < row1 ? row : row1 - 1;
+        __builtin_amdgcn_global_load_lds(codes + row * 128 + (doff[i] & 127),
+                                         (__attribute__((address_space(3))) void*)(buf + (w * GPW + i) * 1024), 16, 0, 0);
+      }
     }
   };
   const uint32_t pk0 = lds_addr(pk), ub0 = lds_addr(ub), pcr0 = lds_addr(pcr);
-  const uint32_t lc0 = lds_addr(lcnt), stg0 = lds_addr(stg);
+  const uint32_t lc0 = lds_addr(lcnt), tq0 = lds_addr(tq), stg0 = lds_addr(stg);
   // unit u of this wave = (nblk, piece) = ((4w+u) >> 3, (4w+u) & 7): lane -> tile row
   // 32*nblk + ri; piece p (dwords 4p..4p+3) holds k-steps 2p, 2p+1; lane-half h takes dword
-  // 2j+h of step 2p+j.  Unpacked layout [n-block][k-step][lane][16 B]: group g = 16*nblk + s.
+  // 4p+2h of step 2p and 4p+2h+1 of step 2p+1 (one 8-byte read per lane).  Unpacked layout
+  // [n-block][k-step][lane][16 B]: group g = 16*nblk + s.
   uint32_t usrc[4], udst[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int unit = 4 * w + u, nblk = unit >> 3, p = unit & 7;
     const int r = nblk * 32 + ri;
-    usrc[u] = (uint32_t)(pk_slot(r, p) * 16);
+    usrc[u] = (uint32_t)(pk_slot(r, p) * 16 + h * 8);
     udst[u] = (uint32_t)(((nblk * KS + 2 * p) * 64 + l) * 16);
   }
   // row popcounts: tile rows 16w..16w+15, 4 lanes per row, 2 pieces each
   const int pr = 16 * w + (l >> 2), pc0 = 2 * (l & 3);
   const uint32_t psrc0 = (uint32_t)(pk_slot(pr, pc0) * 16), psrc1 = (uint32_t)(pk_slot(pr, pc0 + 1) * 16);
-  auto unpack_write = [&](const v4i& v, int u, uint32_t ubuf) {
-    lds_write128(ubuf + udst[u], unpack32((uint32_t)(h ? v.y : v.x)));
-    lds_write128(ubuf + udst[u] + 1024, unpack32((uint32_t)(h ? v.w : v.z)));
+  auto unpack_write = [&](const v2i& v, int u, uint32_t ubuf) __attribute__((always_inline)) {
+    lds_write128(ubuf + udst[u], unpack_row32((uint32_t)v.x));
+    lds_write128(ubuf + udst[u] + 1024, unpack_row32((uint32_t)v.y));
   };
-  auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) {
+  auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) __attribute__((always_inline)) {
     int pc = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(c.x) + __popc(c.y) + __popc(c.z) +
              __popc(c.w);
     pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
@@ -196,13 +243,13 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     if ((l & 3) == 0) lds_write32(pbuf + (uint32_t)(pr * 4), pc);
   };
 
-  // ---- prologue: DMA tiles 0..3, A fragments + thresholds, unpack tiles 0 and 1 ----
+  // ---- prologue: DMA tiles 0..NPK-1, A fragments + thresholds, unpack tiles 0 and 1 ----
   for (int t = 0; t < NPK && t < ntiles; ++t) issue(t);
 
   const int qbase = qb * QPB + w * QPW;
-  v4i A[2][KS];  // [m][s]: bits 64s+32h .. +31 of query qbase + 32m + ri as 32 e2m1 values
+  v4i A[MB][KS];  // [m][s]: bits 64s+32h .. +31 of query qbase + 32m + ri as 32 e2m1 values
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
+  for (int m = 0; m < MB; ++m) {
     const int q = qbase + 32 * m + ri;
     const bool qok = q < nq && (!rerun || rerun[q]);
     const uint4* qp = reinterpret_cast<const uint4*>(queries + (int64_t)(qok ? q : 0) * 128);
@@ -212,46 +259,63 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       const uint4 v = qp[c];
       const uint32_t wd[4] = {qok ? v.x : 0u, qok ? v.y : 0u, qok ? v.z : 0u, qok ? v.w : 0u};
       pc += __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
-      A[m][2 * c] = unpack32(h ? wd[1] : wd[0]);
-      A[m][2 * c + 1] = unpack32(h ? wd[3] : wd[2]);
+      A[m][2 * c] = unpack_query32(h ? wd[2] : wd[0]);
+      A[m][2 * c + 1] = unpack_query32(h ? wd[3] : wd[1]);
     }
-    // lane (ri, h=0) holds query ri's threshold; slot [m][h'][g] wants query (g&3)+8(g>>2)+4h'.
-    // The wave's staging area holds the 64 thresholds until the first hit.
-    const int tl = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;  // padded queries never accept
-    if (h == 0) {
-      const int g = (ri & 3) | ((ri >> 3) << 2);     // inverse of (g&3) + 8(g>>2)
-      stg[(m * 2 + ((ri >> 2) & 1)) * 16 + g] = tl;
-    }
+    // tau'(q) = tau(q) - pc(q): a row is a candidate iff pc(r) - 2<q,r> < tau'
+    if (h == 0) tq[32 * m + ri] = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;  // padded queries never accept
   }
   // A lives in the accumulator file (the MFMA reads it from there); VGPRs hold the
   // accumulators, seeds and the B ring
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(A[m][s]));
-  lcnt[l] = 0;
+  // accumulator seed tau'/2 per register (register g of lane half h holds query
+  // (g&3) + 8(g>>2) + 4h of the M-block): after the K loop acc = <q,r> + tau'/2, and the row is
+  // a candidate iff pc(r) - 2<q,r> < tau'  <=>  acc > pc(r)/2.  The seeds of M-block m stay in LDS
+  // (sd: [m][h][g] floats, 64 B per lane half: broadcast reads) and are loaded into the
+  // accumulators of an n-block right after that block's epilogue.
+  float* sd = reinterpret_cast<float*>(pcr + NUB * RT + 2 * MWAVES * QPW + MWAVES * (STG + 1)) + w * MB * 32;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+    if (l < 32) {  // lane l writes [m][h = l >> 4][g = l & 15]
+      const int g = l & 15, hh = l >> 4;
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
+    }
+  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64);  // this lane half's 16 seeds of M-block 0
+  auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
+    v4i p0, p1, p2, p3;
+    lds_read128(p0, sd0 + (uint32_t)(m * 128));
+    lds_read128(p1, sd0 + (uint32_t)(m * 128 + 16));
+    lds_read128(p2, sd0 + (uint32_t)(m * 128 + 32));
+    lds_read128(p3, sd0 + (uint32_t)(m * 128 + 48));
+    const v16i x = __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                           __builtin_shufflevector(p2, p3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4,
+                                           5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    a = __builtin_bit_cast(v16f, x);
+  };
+  for (int i = l; i < QPW; i += 64) lcnt[i] = 0;
   __syncthreads();
-  // accumulator seed tau'/2 per register: after the K loop acc = <q,r> + tau'/2, and the row is
-  // a candidate iff pc(r) - 2<q,r> < tau'  <=>  acc > pc(r)/2
-  v16f seed[2];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int g = 0; g < 16; ++g) seed[m][g] = 0.5f * (float)stg[(m * 2 + h) * 16 + g];
-
-  if (ntiles >= 4)
-    wait_vm<2 * GPW>();
-  else if (ntiles == 3)
-    wait_vm<GPW>();
-  else
-    wait_vm<0>();
-  barrier_all();  // packed tiles 0 and 1 visible to all waves; thresholds read
+  // at most k tiles' DMA still in flight (k <= NPK - 2; wave-uniform k)
+  auto wait_tiles = [&](int k) __attribute__((always_inline)) {
+    if (k <= 0) wait_vm<0>();
+    else if (k == 1) wait_vm<GPW>();
+    else if (k == 2) wait_vm<2 * GPW>();
+    else if (k == 3) wait_vm<3 * GPW>();
+    else wait_vm<4 * GPW>();
+  };
+  static_assert(NPK - 2 <= 4, "wait_tiles covers up to 4 tiles in flight");
+  const int nissued = ntiles < NPK ? ntiles : NPK;
+  wait_tiles(nissued - 2);
+  barrier_all();  // packed tiles 0 and 1 visible to all waves
   {
-    v4i pv[8], pa[2], pb[2];
+    v2i pv[8];
+    v4i pa[2], pb[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) lds_read128(pv[4 * t + u], pk0 + (uint32_t)(t * PKT) + usrc[u]);
+      for (int u = 0; u < 4; ++u) lds_read64(pv[4 * t + u], pk0 + (uint32_t)(t * PKT) + usrc[u]);
       lds_read128(pa[t], pk0 + (uint32_t)(t * PKT) + psrc0);
       lds_read128(pb[t], pk0 + (uint32_t)(t * PKT) + psrc1);
     }
@@ -265,10 +329,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       rowpc_write(pa[t], pb[t], pcr0 + (uint32_t)(t * RT * 4));
     }
   }
-  if (ntiles >= 4)
-    wait_vm<GPW>();
-  else
-    wait_vm<0>();
+  wait_tiles(nissued - 3);
   wait_lgkm0();
 
   // ---- hit path ----
@@ -277,26 +338,26 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;
   int nst = 0;  // staged entries (wave-uniform)
   // Staged entries -> per-(query, chunk) lists in HBM.  The first 64 entries of a tile go
-  // asynchronously: read back from the stage in group 22 (all hits of a tile are staged by group
-  // 21), list positions taken by ds_add_rtn in group 26, both in the MFMA shadow; the global
+  // asynchronously: read back from the stage in group 20 + MB (all hits of a tile are staged by
+  // group 19 + MB), list positions taken by ds_add_rtn in group 24 + MB, both in the MFMA shadow; the global
   // stores issue at the top of the next iteration, BEFORE that iteration's LDS-DMA, so the
   // end-of-tile vmcnt wait never waits on a store issued after a DMA.  Entries past 64 (and a
   // stage overflow) take the synchronous path at the end of the tile.
   int fe = 0, fpos = 0, nfl = 0;
   int64_t fbase = 0;
-  auto fkey = [&](int e, int64_t base_row) {
+  auto fkey = [&](int e, int64_t base_row) __attribute__((always_inline)) {
     return ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) | (uint64_t)(base_row + (e & 127));
   };
-  auto store_flushed = [&]() {
+  auto store_flushed = [&]() __attribute__((always_inline)) {
     if (nfl) {
-      const int ql = (fe >> ENT_Q_SHIFT) & 63;
+      const int ql = (fe >> ENT_Q_SHIFT) & 127;
       if (l < nfl && fpos < capc) cbase[ql * qstride + fpos] = fkey(fe, fbase);
       nfl = 0;
     }
   };
-  auto flush_from = [&](int i_begin, int64_t base_row) {
+  auto flush_from = [&](int i_begin, int64_t base_row) __attribute__((always_inline)) {
     if (nst > STG) {  // staging overflowed in this tile: every list of the wave -> exact rescan
-      lds_add32(lc0 + (uint32_t)(l * 4), capc + 1);
+      for (int i = l; i < QPW; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
       nst = STG;
     }
     for (int i0 = i_begin; i0 < nst; i0 += 64) {
@@ -304,132 +365,213 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       int e = 0, pos = 0;
       if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
-      const int ql = (e >> ENT_Q_SHIFT) & 63;
+      const int ql = (e >> ENT_Q_SHIFT) & 127;
       if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
       if (i < nst && pos < capc) cbase[ql * qstride + pos] = fkey(e, base_row);
     }
     nst = 0;
   };
-  // hits of block (m, n-block) whose rows are rel7 = row - (t-1)*64.  A block with a hit sends
-  // all 16 compares out first (VALU -> SGPR lane masks) so the wave pays one VALU->SALU latency
-  // per block, not one per register; registers without hits cost a scalar test.  Positions past STG land in a
-  // spare slot and the flush marks the whole wave's lists overflowed (exact rescan).
-  auto block_hits = [&](const v16f& a, int m, int pc, float hp, int rel7) {
-    if (!any_above(a, hp)) return;  // max3 tree + one compare: most blocks stop here
-    uint64_t mk[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) mk[g] = __ballot(a[g] > hp);
-    VRQ_SCHED_FENCE();  // all compares issue back to back before the first scalar test
+  // hits of block (m, n-block) whose rows are rel7 = row - (t-1)*64.  Blocks without a hit stop at
+  // the max3 tree + one compare; a block with hits (rare: ~0.5 % of blocks at 100M rows) takes one
+  // ballot per register (few live registers: this path is inlined into the MFMA loop).  Positions
+  // past STG land in a spare slot and the flush marks the whole wave's lists overflowed (exact rescan).
+  auto block_hits = [&](const v16f& a, int m, int pc, float hp, int rel7) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      if (mk[g]) {
-        const uint64_t mask = mk[g];
+      const uint64_t mask = __ballot(a[g] > hp);
+      if (mask) {
         if ((mask >> l) & 1) {
           const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-          const int v = pc - 2 * (int)(a[g] - seed[m][g]);  // exact integers
-          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+          // lane-dependent values of this rare path are derived from an opaque copy of the lane
+          // id, so loop-invariant code motion cannot hoist them into registers held by the loop
+          int lo = l;
+          asm volatile("" : "+v"(lo));
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+          int tql;  // tau'(q): acc = <q,r> + tau'/2
+          lds_read32(tql, tq0 + (uint32_t)(ql * 4));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tql)::"memory");
+          const int v = pc - (int)(2.0f * a[g]) + tql;  // dist - pc(q): exact integers
           const int pos = nst + below < STG ? nst + below : STG;
-          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | rel7);
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
         }
         nst += __popcll(mask);
       }
     }
   };
-  auto row_pc = [&](int pcv, int lr) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
+  auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
   // DENSE: all 16 distances of block (m, n-block) -> dv (row lr of the chunk)
-  auto block_dense = [&](const v16f& a, int m, int pc, int lr) {
+  auto block_dense = [&](const v16f& a, int m, int pc, int lr) __attribute__((always_inline)) {
     const int64_t col = (int64_t)chunk * chunk_rows + lr;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-      const int v = pc - 2 * (int)a[g];
+      const int v = pc - (int)(2.0f * a[g]);
       if (q < nq) dv[(int64_t)q * dv_stride + col] = lr < nrows ? (uint16_t)(v + 1024) : (uint16_t)0xFFFF;
     }
   };
 
-  // ---- main loop: 32 groups per tile; group gi = (n-block gi>>4, k-step gi&15) runs the two
-  // MFMAs of M-blocks 0 and 1 on ONE B fragment (read BAHEAD groups ahead into a ring of 4,
-  // across the tile boundary: tile t+1 is complete before iteration t starts).  Unpack of tile
-  // t+2 (one unit per 8 groups) and the epilogue of the previous n-block run in the MFMA shadow.
+  // ---- main loop: 32 groups per tile (schedule above) ----
   v4i ring[NRING];
-  v16f acc[2][2];  // [n-block][m]
-  auto readB = [&](int slot_, uint32_t ubuf, int g) { lds_read128(ring[slot_], ubuf + (uint32_t)((g * 64 + l) * 16)); };
+  const uint32_t bl0 = ub0 + (uint32_t)(l * 16);  // + tile slot + group * 1024: this lane's B fragment
   int pcvP = 0;  // previous tile's n-block 1 row popcount
+  uint64_t hitm = 0;  // lanes of the previous n-block with a candidate in some M-block (wave-uniform)
+  int hpb = 0;   // the previous n-block's per-lane threshold pc(r)/2, as float bits
+  v16f acc[2][MB];  // [n-block][m]
+  if constexpr (!DENSE)
+    static_for<0, MB>([&](auto M) {
+      constexpr int m = decltype(M)::value;
+      load_seed(acc[0][m], m);
+      load_seed(acc[1][m], m);
+    });
   barrier_all();  // B_0: unpacked tiles 0 and 1, packed tile 2 visible
-#pragma unroll
-  for (int g = 0; g < BAHEAD; ++g) readB(g, ub0, g);
+  static_for<0, BAHEAD>([&](auto G) {
+    constexpr int g = decltype(G)::value;
+    lds_read128_imm<g * 1024>(ring[g], bl0);
+  });
   for (int t = 0; t < ntiles; ++t) {
-    store_flushed();                   // previous tile's first 64 hits
-    if (t + 4 < ntiles) issue(t + 4);  // into the slot of tile t (unpacked in iteration t-2)
-    const uint32_t ubt = ub0 + (uint32_t)((t % NUB) * UBT);
-    const uint32_t ubn = ub0 + (uint32_t)(((t + 1) % NUB) * UBT);
+    store_flushed();                       // previous tile's first 64 hits
+    if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
+    const uint32_t blt = bl0 + (uint32_t)((t % NUB) * UBT);
+    const uint32_t bln = bl0 + (uint32_t)(((t + 1) % NUB) * UBT);
     const uint32_t ubw = ub0 + (uint32_t)(((t + 2) % NUB) * UBT);
     const uint32_t pks = pk0 + (uint32_t)(((t + 2) % NPK) * PKT);
     int pcv[2];
     lds_read32(pcv[0], pcr0 + (uint32_t)(((t % NUB) * RT + ri) * 4));
     lds_read32(pcv[1], pcr0 + (uint32_t)(((t % NUB) * RT + 32 + ri) * 4));
-    v4i pv, pa, pb;
+    v2i pv;
+    v4i pa, pb;
     VRQ_SCHED_FENCE();
     static_for<0, NG>([&](auto GI) {
       constexpr int gi = decltype(GI)::value;
       constexpr int nbk = gi >> 4, s = gi & 15, j = gi & 15;
       if constexpr (gi + BAHEAD < NG)
-        readB((gi + BAHEAD) & (NRING - 1), ubt, gi + BAHEAD);
+        lds_read128_imm<(gi + BAHEAD) * 1024>(ring[(gi + BAHEAD) & (NRING - 1)], blt);
       else
-        readB((gi + BAHEAD) & (NRING - 1), ubn, gi + BAHEAD - NG);
-      // packed reads of the unpack units (used 4 groups later) and of the row popcounts
-      if ((gi & 7) == 1) lds_read128(pv, pks + usrc[gi >> 3]);
-      if (gi == 26) {
+        lds_read128_imm<(gi + BAHEAD - NG) * 1024>(ring[(gi + BAHEAD) & (NRING - 1)], bln);
+      // packed reads of the unpack units (used 5 groups later) and of the row popcounts
+      if constexpr ((gi & 7) == 1) lds_read64(pv, pks + usrc[gi >> 3]);
+      if constexpr (gi == 12) {
         lds_read128(pa, pks + psrc0);
         lds_read128(pb, pks + psrc1);
       }
       // everything but the BAHEAD most recent LDS operations has completed: the fragment of
-      // this group (read BAHEAD groups ago), the packed unit read 4 groups ago, the popcounts
+      // this group (read BAHEAD groups ago), the packed unit read 5 groups ago, the popcounts
       asm volatile(VRQ_BWAIT
                    : "+v"(ring[gi & (NRING - 1)]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb), "+v"(fe)
                    : "n"(BAHEAD)
                    : "memory");
-      if (!(VRQ_BISECT & 4)) {
-        acc[nbk][0] = mfma_fp4(A[0][s], ring[gi & (NRING - 1)], s == 0 ? seed[0] : acc[nbk][0]);
-        acc[nbk][1] = mfma_fp4(A[1][s], ring[gi & (NRING - 1)], s == 0 ? seed[1] : acc[nbk][1]);
-      } else if (s == 0) {
-        acc[nbk][0] = seed[0];
-        acc[nbk][1] = seed[1];
-      }
-      // pin the accumulators here: the MFMA intrinsics are pure, and without a use at this
-      // point IR-level sinking moves them past the scheduling fences
-      asm volatile("" : "+v"(acc[nbk][0]), "+v"(acc[nbk][1]));
-      if ((gi & 7) == 5 && !(VRQ_BISECT & 2)) unpack_write(pv, gi >> 3, ubw);
-      if constexpr (gi == 22 && !DENSE) {  // async flush, step 1: the stage's first 64 entries
-        lds_read32(fe, stg0 + (uint32_t)(l * 4));
-        nfl = nst < 64 ? nst : 64;
-      }
-      if constexpr (gi == 26 && !DENSE)  // step 2: list positions (idle lanes add 0)
-        lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 63) * 4), l < nfl ? 1 : 0);
-      if (gi == 30 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
-      // epilogue of the previous n-block (n-block 1 of tile t-1 during n-block 0, n-block 0 of
-      // tile t during n-block 1): any-tests in group 3, hits of (m, register half) in 4..7
-      if (!(VRQ_BISECT & 1) && (j == 3 || j == 5) && (nbk == 1 || t > 0)) {
-        const v16f* pa_ = acc[nbk ^ 1];
-        const int pcr_ = nbk == 0 ? pcvP : pcv[0];
-        const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
-        const int pc = row_pc(pcr_, lr);
-        constexpr int m = j == 3 ? 0 : 1;
-        if constexpr (DENSE)
-          block_dense(pa_[m], m, pcr_, lr);
-        else
-          block_hits(pa_[m], m, pc, 0.5f * (float)pc, (nbk == 0 ? 32 : 64) + ri);
-      }
+      // The group's non-MFMA work is cut into four slots that sit between its MFMAs (slot k after
+      // MFMA k; at MB = 2 slots 2k and 2k+1 after MFMA k): an in-order wave issues them while the
+      // matrix core runs, instead of one burst after the last MFMA of the group.
+      //   slot 0: hit test part 1 (three max3), unpack low half, seeds of M-block m0
+      //   slot 1: hit test part 2 (three max3), unpack high half, seeds of M-block m0 + 1
+      //   slot 2: hit test part 3 (max3, max, compare -> flag), row popcounts, sample-pass stores
+      //   slot 3: asynchronous flush steps, the n-block's (rare) hit-extraction branch
+      constexpr bool TEST = !(VRQ_BISECT & 1) && !DENSE && j >= 2 && j < 2 + MB;
+      constexpr int tm = TEST ? j - 2 : 0;
+      int e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, f0 = 0;
+      auto slot = [&](auto K) __attribute__((always_inline)) {
+        constexpr int k = decltype(K)::value;
+        if constexpr (k == 0) {
+          if constexpr (TEST) {
+            if constexpr (tm == 0) {  // the n-block's threshold pc(r)/2 (bit pattern, >= 0)
+              const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+              const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+              // (no previous n-block before tile 0: a threshold no accumulator exceeds)
+              hpb = (nbk == 0 && t == 0) ? 0x7fffffff : __float_as_int(0.5f * (float)row_pc(pcr_, lr));
+            }
+            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
+            e0 = max(max(bb[0], bb[1]), bb[2]);
+            e1 = max(max(bb[3], bb[4]), bb[5]);
+            e2 = max(max(bb[6], bb[7]), bb[8]);
+            asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(hpb));
+          }
+          if constexpr ((gi & 7) == 6 && !(VRQ_BISECT & 2))
+            lds_write128(ubw + udst[gi >> 3], unpack_row32((uint32_t)pv.x));
+          if constexpr (!DENSE && j == 4 + MB) load_seed(acc[nbk ^ 1][0], 0);
+          if constexpr (!DENSE && j == 5 + MB && MB > 2) load_seed(acc[nbk ^ 1][2], 2);
+        } else if constexpr (k == 1) {
+          if constexpr (TEST) {
+            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
+            e3 = max(max(bb[9], bb[10]), bb[11]);
+            e4 = max(max(bb[12], bb[13]), bb[14]);
+            f0 = max(max(e0, e1), e2);
+            asm volatile("" : "+v"(e3), "+v"(e4), "+v"(f0));
+          }
+          if constexpr ((gi & 7) == 6 && !(VRQ_BISECT & 2))
+            lds_write128(ubw + udst[gi >> 3] + 1024, unpack_row32((uint32_t)pv.y));
+          if constexpr (!DENSE && j == 4 + MB) load_seed(acc[nbk ^ 1][1], 1);
+          if constexpr (!DENSE && j == 5 + MB && MB > 2) load_seed(acc[nbk ^ 1][3], 3);
+        } else if constexpr (k == 2) {
+          if constexpr (TEST) {
+            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
+            const int f1 = max(max(e3, e4), bb[15]);
+            hitm |= __ballot(max(f0, f1) > hpb);
+          }
+          if constexpr (gi == 28 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
+          if constexpr (DENSE && !(VRQ_BISECT & 1) && j >= 2 && j < 2 + MB) {
+            if (nbk == 1 || t > 0) {
+              const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+              const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+              block_dense(acc[nbk ^ 1][j - 2], j - 2, pcr_, lr);
+            }
+          }
+        } else {
+          // async flush, step 1 (after the last hit extraction of the tile, group 16 + 3 + MB): the
+          // stage's first 64 entries; step 2, four groups (>= 4 LDS operations) later: list positions
+          if constexpr (gi == 20 + MB && !DENSE) {
+            lds_read32(fe, stg0 + (uint32_t)(l * 4));
+            nfl = nst < 64 ? nst : 64;
+          }
+          if constexpr (gi == 24 + MB && !DENSE)  // step 2 (idle lanes add 0)
+            lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 127) * 4), l < nfl ? 1 : 0);
+          // hit extraction of the previous n-block's flagged M-blocks, once per n-block (rare)
+          if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 3 + MB) {
+            if (hitm) {
+              const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+              const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+              const int pc = row_pc(pcr_, lr);
+              const float hp = 0.5f * (float)pc;
+              static_for<0, MB>([&](auto M) {
+                constexpr int mm = decltype(M)::value;
+                if (any_above(acc[nbk ^ 1][mm], hp))
+                  block_hits(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
+              });
+            }
+            hitm = 0;
+          }
+        }
+      };
+      static_for<0, MB>([&](auto M) {
+        constexpr int m = decltype(M)::value;
+        if constexpr (s == 0 && !DENSE)  // the seeds loaded after the block's last epilogue have landed
+          asm volatile("" : "+v"(acc[nbk][m]));
+        if constexpr (!(VRQ_BISECT & 4))
+          acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], (s == 0 && DENSE) ? v16f{} : acc[nbk][m]);
+        else if constexpr (s == 0 && DENSE)
+          acc[nbk][m] = v16f{};
+        // pin the accumulator here: the MFMA intrinsics are pure, and without a use at this
+        // point IR-level sinking moves them past the scheduling fences
+        asm volatile("" : "+v"(acc[nbk][m]));
+        VRQ_SCHED_FENCE();
+        if constexpr (MB == 4) {
+          slot(std::integral_constant<int, m>{});
+        } else {
+          slot(std::integral_constant<int, 2 * m>{});
+          slot(std::integral_constant<int, 2 * m + 1>{});
+        }
+        VRQ_SCHED_FENCE();
+      });
       VRQ_SCHED_FENCE();
     });
     pcvP = pcv[1];
     // packed tile t+3 (unpacked next iteration) landed; this wave's LDS writes done
-    if (t + 4 < ntiles)
-      wait_vm<GPW>();
-    else
-      wait_vm<0>();
+    {
+      const int last = t + NPK < ntiles ? t + NPK : ntiles - 1;  // last tile issued so far
+      wait_tiles(last - (t + 3));
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fpos), "+v"(fe)::"memory");
     fbase = row0 + (int64_t)(t - 1) * RT;
     if (nst > 64) flush_from(64, fbase);  // rare: more than 64 hits in one tile
@@ -441,18 +583,21 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const int lr = (ntiles - 1) * RT + 32 + ri;
     const int pc = row_pc(pcvP, lr);
     const float hp = 0.5f * (float)pc;
-    if constexpr (DENSE) {
-      block_dense(acc[1][0], 0, pcvP, lr);
-      block_dense(acc[1][1], 1, pcvP, lr);
-    } else {
-      block_hits(acc[1][0], 0, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
-      block_hits(acc[1][1], 1, pc, hp, 96 + ri);
-    }
+    static_for<0, MB>([&](auto M) {
+      constexpr int m = decltype(M)::value;
+      if constexpr (DENSE)
+        block_dense(acc[1][m], m, pcvP, lr);
+      else
+        if (any_above(acc[1][m], hp)) block_hits(acc[1][m], m, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
+    });
     if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }
   wait_lgkm0();
-  const int q = qbase + l;
-  if (!DENSE && q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[l];
+  if (!DENSE)
+    for (int i = l; i < QPW; i += 64) {
+      const int q = qbase + i;
+      if (q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[i];
+    }
 }
 
 // Thresholds from the dense sample (S rows spread over the corpus, every distance exact):
@@ -534,7 +679,7 @@ __global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __re
 // exact top-K.  Otherwise the query is flagged for the re-run with tau_p.  One wave per query.
 __global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __restrict__ ccnt, int nchunks, int K,
                                                            int nq, int32_t* __restrict__ rerun,
-                                                           int32_t* __restrict__ qbflag) {
+                                                           int32_t* __restrict__ qbflag, int qpb) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
   if (q >= nq) return;
   int64_t c = 0;
@@ -543,7 +688,7 @@ __global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __rest
   const bool fail = c < K;
   if (l == 0) {
     rerun[q] = fail ? 1 : 0;
-    if (fail) atomicOr(&qbflag[q / QPB], 1);
+    if (fail) atomicOr(&qbflag[q / qpb], 1);
   }
 }
 
@@ -766,7 +911,13 @@ static int sample_order(double lam, int K) {
 
 int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   if (nq < 1 || K < 1 || K > kMfmaMaxK) return VRQ_EUNSUPPORTED;
-  p->nqb = (nq + QPB - 1) / QPB;
+  // VRQ_MFMA_MB: tuning override of the M-blocks per wave (2 or 4; read per call, no state)
+  const char* em = getenv("VRQ_MFMA_MB");
+  p->mb = em && (atoi(em) == 2 || atoi(em) == 4) ? atoi(em) : nq >= kMbLargeMinQueries ? kMbLarge : kMbSmall;
+  p->qpb = p->mb == kMbLarge ? MfmaShape<kMbLarge>::QPB : MfmaShape<kMbSmall>::QPB;
+  p->nqb = (nq + p->qpb - 1) / p->qpb;
+  // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
+  p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
   // sample: nsc chunks of RT-aligned rows spread evenly over [0, n), S rows in total.
   // VRQ_SAMPLE_DIV: tuning override of the sample fraction (read per call, no state)
   const char* ev = getenv("VRQ_SAMPLE_DIV");
@@ -774,7 +925,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   int64_t S = n / div;
   if (S < kMfmaMinSample) S = kMfmaMinSample;
   if (S > n) S = n;
-  int64_t nsc = 256 / p->nqb;  // one workgroup per CU
+  int64_t nsc = 256 / p->nqb_s;  // one workgroup per CU
   if (nsc < 1) nsc = 1;
   int64_t scr = ((S + nsc - 1) / nsc + RT - 1) / RT * RT;
   nsc = (S + scr - 1) / scr;
@@ -829,30 +980,39 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   int32_t* qbflag = (int32_t*)(ws + p.off_tau + 3 * qa);
   const bool sampled = p.j < K;
   const int32_t* none = nullptr;
+  // the MB = 4 or MB = 2 instance of a pass
+  auto pass = [&](auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd, int32_t* cc, int64_t crows,
+                  int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d, int64_t dstride) {
+    if (p.mb == kMbLarge)
+      hipLaunchKernelGGL(kern4, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
+                         crows, cstride, nch, p.nqb, rr, qf, d, dstride);
+    else
+      hipLaunchKernelGGL(kern2, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
+                         crows, cstride, nch, p.nqb, rr, qf, d, dstride);
+  };
   if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
-    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_SAMPLE>, dim3(p.sample_chunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
-                       (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0, p.sample_chunk_rows,
-                       p.sample_stride, p.sample_chunks, p.nqb, none, none, dv, p.sample);
+    hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
+                       0, s, codes, n, (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0,
+                       p.sample_chunk_rows, p.sample_stride, p.sample_chunks, p.nqb_s, none, none, dv, p.sample);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
                        tau_s, tau_p, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_SCAN_STAGE_MATRIX) {
-    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_MAIN>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
-                       (int64_t)0, q, nq, (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.capc,
-                       p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb, none, none, (uint16_t*)nullptr, (int64_t)0);
+    pass(hamming_mfma_kernel<MFMA_MAIN, kMbLarge>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
+         (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
+         (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_RECHECK) && sampled) {
     // prove C >= K per query; re-run the query blocks holding a failed query with tau_p
     hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, (const int32_t*)ccnt, p.nchunks, K,
-                       nq, rerun, qbflag);
+                       nq, rerun, qbflag, p.qpb);
     VRQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(hamming_mfma_kernel<MFMA_RERUN>, dim3(p.nchunks * p.nqb), dim3(MWAVES * 64), 0, s, codes, n,
-                       (int64_t)0, q, nq, (const int32_t*)tau_p, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows,
-                       p.nchunks, p.nqb, (const int32_t*)rerun, (const int32_t*)qbflag, (uint16_t*)nullptr,
-                       (int64_t)0);
+    pass(hamming_mfma_kernel<MFMA_RERUN, kMbLarge>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
+         (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
+         (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_SCAN_STAGE_SUFFIX) {  // candidates of the whole corpus -> one sorted K-list per query

@@ -9,6 +9,7 @@
 
 namespace vrq {
 
+typedef int v2i __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
@@ -44,6 +45,9 @@ __device__ __forceinline__ void lds_read128(v4i& d, uint32_t a) {
 template <int OFF>
 __device__ __forceinline__ void lds_read128_imm(v4i& d, uint32_t a) {  // address + immediate offset
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+__device__ __forceinline__ void lds_read64(v2i& d, uint32_t a) {
+  asm volatile("ds_read_b64 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
 __device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(d) : "v"(a) : "memory");

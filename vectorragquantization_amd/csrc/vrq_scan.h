@@ -44,7 +44,10 @@ struct MfmaPlan {
   int sample_chunks;
   int j;                     // sampled threshold order (tau_s = d_(j) + 1); K = tau_p only
   int capc;                  // candidate capacity per (query, chunk) list
-  int nqb;                   // 256-query blocks
+  int mb;                    // M-blocks (32 queries) per wave of the matrix kernel: 4 or 2
+  int qpb;                   // queries per workgroup (128 * mb)
+  int nqb;                   // query blocks of the thresholded pass
+  int nqb_s;                 // query blocks of the dense sample pass (always the MB = 2 kernel)
   int64_t chunk_rows;        // rows per workgroup of the thresholded pass (multiple of 64)
   int nchunks;
   size_t off_suffix, off_cand, off_cnt, off_tau, bytes;
