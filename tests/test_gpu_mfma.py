@@ -185,16 +185,16 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib):
 
 
 def _sample_rows(n, nq):
-    """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S =
-    max(n/32, 32768) rows in 256/nqb chunks of RT-aligned rows, chunk c at row c * (n // chunks)."""
+    """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S = n/32 rows
+    clamped to [32768, 2^20], as 64-row tiles spread at a tile stride ts >= 64 over the corpus, in
+    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass)."""
     nqb = (nq + 255) // 256
-    S = min(n, max(n // 32, 32768))
-    nsc = max(1, 256 // nqb)
-    scr = ((S + nsc - 1) // nsc + 63) // 64 * 64
-    nsc = (S + scr - 1) // scr
-    stride = n // nsc
-    r = np.arange(n)
-    return r[((r % stride) < scr) & (r // stride < nsc)]
+    S = min(max(n // 32, 32768), 1 << 20) if n // 32 <= (1 << 20) else 1 << 20
+    tiles = min(max(S // 64, 1), n // 64)
+    nsc = min(max(1, 256 // nqb), tiles)
+    tiles = nsc * (tiles // nsc)
+    ts = (n - 64) // (tiles - 1) if tiles > 1 else 64
+    return (np.arange(tiles)[:, None] * ts + np.arange(64)[None, :]).reshape(-1)
 
 
 def test_mfma_sampled_threshold_rerun(dev, oracle_lib):

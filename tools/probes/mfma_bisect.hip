@@ -41,11 +41,11 @@ int main(int argc, char** argv) {
     (void)hipEventRecord(e0, 0);
     if (p.mb == 4)
       hipLaunchKernelGGL((vrq::hamming_mfma_kernel<vrq::MFMA_MAIN, 4>), dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0,
-                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks,
+                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, (int64_t)vrq::RT, p.nchunks,
                          p.nqb, (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
     else
       hipLaunchKernelGGL((vrq::hamming_mfma_kernel<vrq::MFMA_MAIN, 2>), dim3(p.nchunks * p.nqb), dim3(vrq::MWAVES * 64), 0,
-                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks,
+                         0, codes, n, (int64_t)0, q, nq, tau, cand, ccnt, p.capc, p.chunk_rows, p.chunk_rows, (int64_t)vrq::RT, p.nchunks,
                          p.nqb, (const int32_t*)nullptr, (const int32_t*)nullptr, (uint16_t*)nullptr, (int64_t)0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);

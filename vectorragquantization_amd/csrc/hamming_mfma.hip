@@ -135,9 +135,10 @@ __device__ __forceinline__ bool any_above(const v16f& a, float thr) {
 constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7;
 
 // DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) is written
-// as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + row].  Chunk c covers
-// rows [row_begin + c * chunk_stride, + chunk_rows) (the sample spreads its chunks over the corpus;
-// the thresholded pass uses chunk_stride = chunk_rows).
+// as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + local row].  Chunk c
+// starts at row row_begin + c * chunk_stride and its tile t at + t * tile_stride: the sample pass
+// spreads 64-row tiles evenly over the whole corpus (tile_stride >= 64, chunk_rows = its tiles x 64
+// dv columns); the thresholded pass uses chunk_stride = chunk_rows and tile_stride = 64.
 // MODE: MFMA_MAIN (thresholded pass), MFMA_SAMPLE (dense sample pass, DENSE below) or MFMA_RERUN
 // (the exact re-run of failed query blocks: same code as MAIN, a separate symbol so profiles and
 // traces tell the two launches apart).
@@ -155,7 +156,8 @@ template <int MODE, int MB>
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
-    int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, const int32_t* __restrict__ rerun,
+    int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, int nqb,
+    const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
   constexpr int QPW = MfmaShape<MB>::QPW, QPB = MfmaShape<MB>::QPB;
@@ -180,9 +182,12 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // re-run pass (exact fallback of the sampled threshold): only query blocks with a failed query
   if (qbflag && qbflag[qb] == 0) return;
   const int64_t row0 = row_begin + (int64_t)chunk * chunk_stride;
-  const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  // strided (sample pass): tile t starts at row0 + t * tile_stride, every tile whole (the plan keeps
+  // the last one inside the corpus); otherwise the chunk is rows [row0, row0 + chunk_rows)
+  const bool strided = tile_stride != RT;
+  const int64_t row1 = strided ? n : (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
   if (row0 >= row1) return;
-  const int nrows = (int)(row1 - row0);
+  const int nrows = strided ? (int)chunk_rows : (int)(row1 - row0);
   const int ntiles = (nrows + RT - 1) / RT;
 
   // LDS-DMA of packed tile t: this wave's GPW pieces of 64 x 16 B (lane -> (row, piece) through the
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   }
   auto issue = [&](int t) __attribute__((always_inline)) {
     uint8_t* buf = pk + (t % NPK) * PKT;
-    const int64_t tr0 = row0 + (int64_t)t * RT;
+    const int64_t tr0 = row0 + (int64_t)t * tile_stride;
     if (tr0 + RT <= row1) {
       const uint8_t* base = codes + tr0 * 128;
 #pragma unroll
@@ -918,21 +923,30 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->nqb = (nq + p->qpb - 1) / p->qpb;
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
-  // sample: nsc chunks of RT-aligned rows spread evenly over [0, n), S rows in total.
+  // sample: S rows in 64-row tiles spread evenly over the corpus at a tile stride ts >= 64 (a sample
+  // robust to corpora stored in cluster order), in nsc chunks (one workgroup per CU and query block)
+  // of T tiles: tile i = c*T + t starts at row i * ts, the last one inside [0, n).  S = n/32, at least
+  // kMfmaMinSample and at most kMfmaMaxSample rows (the dense pass and its selection cost O(nq S)).
   // VRQ_SAMPLE_DIV: tuning override of the sample fraction (read per call, no state)
   const char* ev = getenv("VRQ_SAMPLE_DIV");
   const int64_t div = ev && atoi(ev) >= 2 ? atoi(ev) : kMfmaSampleDiv;
   int64_t S = n / div;
+  if (S > kMfmaMaxSample) S = kMfmaMaxSample;
   if (S < kMfmaMinSample) S = kMfmaMinSample;
-  if (S > n) S = n;
-  int64_t nsc = 256 / p->nqb_s;  // one workgroup per CU
+  int64_t tiles = S / RT > 0 ? S / RT : 1;
+  if (tiles > n / RT) tiles = n / RT;  // non-overlapping whole tiles (n >= kMfmaMinRows)
+  int64_t nsc = 256 / p->nqb_s;
   if (nsc < 1) nsc = 1;
-  int64_t scr = ((S + nsc - 1) / nsc + RT - 1) / RT * RT;
-  nsc = (S + scr - 1) / scr;
-  p->sample_chunk_rows = scr;
+  if (nsc > tiles) nsc = tiles;
+  const int64_t T = tiles / nsc;
+  tiles = nsc * T;
+  const int64_t ts = tiles > 1 ? (n - RT) / (tiles - 1) : RT;  // >= RT since (tiles - 1) * RT <= n - RT
+  p->sample_chunk_rows = T * RT;
   p->sample_chunks = (int)nsc;
-  p->sample_stride = n / nsc;  // >= scr since S <= n
-  p->sample = nsc * scr;       // dv columns (rows past n are marked invalid)
+  p->sample_stride = T * ts;
+  p->sample_tile_stride = ts;
+  p->sample = tiles * RT;  // dv columns = sample rows
+  S = p->sample;
   // thresholded pass over all n rows
   int64_t want = 256 / p->nqb;
   if (want < 1) want = 1;
@@ -985,15 +999,16 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                   int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d, int64_t dstride) {
     if (p.mb == kMbLarge)
       hipLaunchKernelGGL(kern4, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
-                         crows, cstride, nch, p.nqb, rr, qf, d, dstride);
+                         crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
     else
       hipLaunchKernelGGL(kern2, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
-                         crows, cstride, nch, p.nqb, rr, qf, d, dstride);
+                         crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
   };
   if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
     hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
                        0, s, codes, n, (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0,
-                       p.sample_chunk_rows, p.sample_stride, p.sample_chunks, p.nqb_s, none, none, dv, p.sample);
+                       p.sample_chunk_rows, p.sample_stride, p.sample_tile_stride, p.sample_chunks, p.nqb_s, none,
+                       none, dv, p.sample);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
                        tau_s, tau_p, qbflag, p.nqb);

@@ -33,6 +33,7 @@ int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, cons
 // ---- K1m: matrix-core scan for large query batches (hamming_mfma.hip) ----
 constexpr int kMfmaMaxK = 128;           // K bound of the path
 constexpr int64_t kMfmaMinSample = 32768;
+constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~1.3 ms at nq = 1024)
 constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
 constexpr int kMfmaMinQueries = 128;     // auto-selection threshold on the batch size
 constexpr int64_t kMfmaSampleDiv = 32;   // dense threshold sample = n / kMfmaSampleDiv rows
@@ -41,6 +42,7 @@ struct MfmaPlan {
   int64_t sample;            // dense sample columns (sample_chunks * sample_chunk_rows)
   int64_t sample_chunk_rows;
   int64_t sample_stride;     // sample chunk c starts at row c * sample_stride
+  int64_t sample_tile_stride;  // rows between consecutive sample tiles (>= 64)
   int sample_chunks;
   int j;                     // sampled threshold order (tau_s = d_(j) + 1); K = tau_p only
   int capc;                  // candidate capacity per (query, chunk) list
