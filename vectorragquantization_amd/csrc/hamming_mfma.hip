@@ -469,61 +469,101 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
                    : "memory");
       // The group's non-MFMA work is cut into four slots that sit between its MFMAs (slot k after
       // MFMA k; at MB = 2 slots 2k and 2k+1 after MFMA k): an in-order wave issues them while the
-      // matrix core runs, instead of one burst after the last MFMA of the group.
-      //   slot 0: hit test part 1 (three max3), unpack low half, seeds of M-block m0
-      //   slot 1: hit test part 2 (three max3), unpack high half, seeds of M-block m0 + 1
-      //   slot 2: hit test part 3 (max3, max, compare -> flag), row popcounts, sample-pass stores
-      //   slot 3: asynchronous flush steps, the n-block's (rare) hit-extraction branch
+      // matrix core runs, at most ~3 vector instructions per slot, instead of one burst after the
+      // last MFMA of the group.  Per group kind:
+      //   hit test of M-block m (j = 2+m): max3 pairs in slots 0-2, the last max3 + compare in 3
+      //   the n-block threshold pc(r)/2 (j = 1), the (rare) hit-extraction branch (j = 3+MB, slot 3)
+      //   unpack of unit u (gi = 8u+6): 3 + 2 ops per dword, the two LDS writes in slots 1 and 3
+      //   row popcounts (gi = 28): 4 + 4 bcnt, the lane-quad sums, the LDS write
+      //   accumulator re-seeds (j = 4+MB .. 3+2MB... one M-block per group, one read per slot)
+      //   asynchronous hit flush (gi = 20+MB and 24+MB, slot 3)
       constexpr bool TEST = !(VRQ_BISECT & 1) && !DENSE && j >= 2 && j < 2 + MB;
       constexpr int tm = TEST ? j - 2 : 0;
+      constexpr bool UNPACK = (gi & 7) == 6 && !(VRQ_BISECT & 2);
+      constexpr bool SEED = !DENSE && j >= 4 + MB && j < 4 + 2 * MB;
+      constexpr int sm = SEED ? j - 4 - MB : 0;
       int e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, f0 = 0;
+      uint32_t u0 = 0, u1 = 0, u2 = 0;
+      int pc0 = 0, pc1 = 0;
       auto slot = [&](auto K) __attribute__((always_inline)) {
         constexpr int k = decltype(K)::value;
-        if constexpr (k == 0) {
-          if constexpr (TEST) {
-            if constexpr (tm == 0) {  // the n-block's threshold pc(r)/2 (bit pattern, >= 0)
-              const int pcr_ = nbk == 0 ? pcvP : pcv[0];
-              const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
-              // (no previous n-block before tile 0: a threshold no accumulator exceeds)
-              hpb = (nbk == 0 && t == 0) ? 0x7fffffff : __float_as_int(0.5f * (float)row_pc(pcr_, lr));
-            }
-            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
+        const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
+        if constexpr (TEST) {
+          if constexpr (k == 0) {
             e0 = max(max(bb[0], bb[1]), bb[2]);
             e1 = max(max(bb[3], bb[4]), bb[5]);
+            asm volatile("" : "+v"(e0), "+v"(e1));
+          } else if constexpr (k == 1) {
             e2 = max(max(bb[6], bb[7]), bb[8]);
-            asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(hpb));
-          }
-          if constexpr ((gi & 7) == 6 && !(VRQ_BISECT & 2))
-            lds_write128(ubw + udst[gi >> 3], unpack_row32((uint32_t)pv.x));
-          if constexpr (!DENSE && j == 4 + MB) load_seed(acc[nbk ^ 1][0], 0);
-          if constexpr (!DENSE && j == 5 + MB && MB > 2) load_seed(acc[nbk ^ 1][2], 2);
-        } else if constexpr (k == 1) {
-          if constexpr (TEST) {
-            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
             e3 = max(max(bb[9], bb[10]), bb[11]);
+            asm volatile("" : "+v"(e2), "+v"(e3));
+          } else if constexpr (k == 2) {
             e4 = max(max(bb[12], bb[13]), bb[14]);
             f0 = max(max(e0, e1), e2);
-            asm volatile("" : "+v"(e3), "+v"(e4), "+v"(f0));
+            asm volatile("" : "+v"(e4), "+v"(f0));
+          } else {
+            hitm |= __ballot(max(max(e3, e4), max(bb[15], f0)) > hpb);
           }
-          if constexpr ((gi & 7) == 6 && !(VRQ_BISECT & 2))
-            lds_write128(ubw + udst[gi >> 3] + 1024, unpack_row32((uint32_t)pv.y));
-          if constexpr (!DENSE && j == 4 + MB) load_seed(acc[nbk ^ 1][1], 1);
-          if constexpr (!DENSE && j == 5 + MB && MB > 2) load_seed(acc[nbk ^ 1][3], 3);
-        } else if constexpr (k == 2) {
-          if constexpr (TEST) {
-            const v16i bb = __builtin_bit_cast(v16i, acc[nbk ^ 1][tm]);
-            const int f1 = max(max(e3, e4), bb[15]);
-            hitm |= __ballot(max(f0, f1) > hpb);
+        }
+        if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 1 && k == 0) {
+          // the n-block's threshold pc(r)/2 as float bits (>= 0); no previous n-block before tile 0:
+          // a threshold no accumulator exceeds
+          const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+          const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+          hpb = (nbk == 0 && t == 0) ? 0x7fffffff : __float_as_int(0.5f * (float)row_pc(pcr_, lr));
+          asm volatile("" : "+v"(hpb));
+        }
+        if constexpr (UNPACK) {  // unpack_row32 of pv.x (slots 0, 1) and pv.y (slots 2, 3)
+          constexpr int half = k >> 1;
+          const uint32_t wv = (uint32_t)(half ? pv.y : pv.x);
+          if constexpr ((k & 1) == 0) {
+            u0 = wv & 0x11111111u;
+            u1 = wv & 0x22222222u;
+            u2 = wv & 0x44444444u;
+            asm volatile("" : "+v"(u0), "+v"(u1), "+v"(u2));
+          } else {
+            v4i r;
+            r.x = (int)u0;
+            r.y = (int)u1;
+            r.z = (int)u2;
+            r.w = (int)((wv >> 1) & 0x44444444u);
+            lds_write128(ubw + udst[gi >> 3] + (uint32_t)(half * 1024), r);
           }
-          if constexpr (gi == 28 && !(VRQ_BISECT & 2)) rowpc_write(pa, pb, pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4));
-          if constexpr (DENSE && !(VRQ_BISECT & 1) && j >= 2 && j < 2 + MB) {
-            if (nbk == 1 || t > 0) {
-              const int pcr_ = nbk == 0 ? pcvP : pcv[0];
-              const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
-              block_dense(acc[nbk ^ 1][j - 2], j - 2, pcr_, lr);
-            }
+        }
+        if constexpr (gi == 28 && !(VRQ_BISECT & 2)) {  // row popcounts of tile t+2
+          if constexpr (k == 0) {
+            pc0 = __popc(pa.x) + __popc(pa.y) + __popc(pa.z) + __popc(pa.w);
+            asm volatile("" : "+v"(pc0));
+          } else if constexpr (k == 1) {
+            pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
+            asm volatile("" : "+v"(pc1));
+          } else if constexpr (k == 2) {
+            pc0 += pc1;
+            pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+            asm volatile("" : "+v"(pc0));
+          } else {
+            pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+            if ((l & 3) == 0) lds_write32(pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4 + pr * 4), pc0);
           }
-        } else {
+        }
+        if constexpr (SEED) {  // one 16-byte piece of M-block sm's seeds per slot, into its accumulator
+          v4i piece;
+          lds_read128(piece, sd0 + (uint32_t)(sm * 128 + k * 16));
+          v16i x = __builtin_bit_cast(v16i, acc[nbk ^ 1][sm]);
+          x[4 * k] = piece.x;
+          x[4 * k + 1] = piece.y;
+          x[4 * k + 2] = piece.z;
+          x[4 * k + 3] = piece.w;
+          acc[nbk ^ 1][sm] = __builtin_bit_cast(v16f, x);
+        }
+        if constexpr (DENSE && !(VRQ_BISECT & 1) && j >= 2 && j < 2 + MB && k == 0) {
+          if (nbk == 1 || t > 0) {
+            const int pcr_ = nbk == 0 ? pcvP : pcv[0];
+            const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
+            block_dense(acc[nbk ^ 1][j - 2], j - 2, pcr_, lr);
+          }
+        }
+        if constexpr (k == 3) {
           // async flush, step 1 (after the last hit extraction of the tile, group 16 + 3 + MB): the
           // stage's first 64 entries; step 2, four groups (>= 4 LDS operations) later: list positions
           if constexpr (gi == 20 + MB && !DENSE) {
