@@ -175,3 +175,41 @@ def test_cohere_vector_db_float_surface(dev, tmp_path):
     db2 = CohereVectorDBFloat(str(tmp_path / "db"), provider=prov, device=dev)
     assert len(db2) == 299
     assert db2.search(docs[3], k=3) == db.search(docs[3], k=3)
+
+
+@pytest.mark.parametrize("order", ["random", "cluster_sorted"])
+def test_flat_ip_1m_clustered_served_without_fallback(dev, monkeypatch, order):
+    """1M clustered rows (4096 clusters of ~244: the dense sample holds only a few rows of a query's
+    cluster, so the sampled threshold admits far more rows than a candidate list holds).  The
+    overflowing queries must be served by the retry pass (threshold raised to the k-th exact score
+    among the recorded candidates), not by the one-workgroup full-scan fallback: VRQ_GEMM_FALLBACK=0
+    makes any fallback query an error.  Exact against a float64 matmul (ties within one f32 ulp).
+    ``cluster_sorted`` stores the rows in cluster order (the sample's chunks then miss most clusters)."""
+    from vectorragquantization_amd.flat import flat_ip_prepare, flat_ip_topk
+    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")
+    g = torch.Generator(device=dev).manual_seed(77)
+    n, nq, k = 1_000_000, 128, 10
+    cent = torch.randn((4096, 1024), generator=g, device=dev)
+    cid = torch.randint(0, 4096, (n,), generator=g, device=dev)
+    if order == "cluster_sorted":
+        cid = torch.sort(cid).values
+    xf = torch.empty((n, 1024), dtype=torch.float32, device=dev)
+    for s0 in range(0, n, 1 << 18):
+        e = min(n, s0 + (1 << 18))
+        b = cent[cid[s0:e]] + 0.7 * torch.randn((e - s0, 1024), generator=g, device=dev)
+        xf[s0:e] = b / b.norm(dim=1, keepdim=True)
+    qi = torch.randint(0, n, (nq,), generator=g, device=dev)
+    qf = xf[qi] + (0.3 / 32.0) * torch.randn((nq, 1024), generator=g, device=dev)
+    qf = (qf / qf.norm(dim=1, keepdim=True)).contiguous()
+    bounds = torch.zeros((2,), dtype=torch.float64, device=dev)
+    x8, inv = flat_ip_prepare(xf, bounds)
+    cnt, rows, sc = flat_ip_topk(xf, x8, inv, bounds, qf, k)
+    torch.cuda.synchronize()
+    assert bool((cnt == k).all())
+    S = (qf.double() @ xf.double().T).float().double()          # the f32-rounded exact dot
+    ref_sc, ref = torch.topk(S, k, dim=1)
+    got = torch.gather(S, 1, rows)
+    ulp = torch.from_numpy(_ulp(ref_sc.cpu().numpy())).to(dev)
+    assert bool((torch.abs(sc - got) <= ulp).all())               # each returned score is its row's
+    assert bool((torch.abs(sc - ref_sc) <= ulp).all())            # the k best values
+    assert bool((torch.diff(sc, dim=1) <= 0).all())

@@ -133,9 +133,11 @@ __device__ __forceinline__ int xcd_logical(int b, int nb) {
 
 // ---------------------------------------------------------------------------------------------
 // prep: one wave per (padded) query.  qa[q] = pieces a, b in fragment order (natural k order for
-// Phase III, ph2_pos for Phase II); delta[q] = Delta_q in u units.
+// Phase III, ph2_pos for Phase II); delta[q] = Delta_q in u units; (alpha[q], beta[q]) map a reference
+// score s to u units (s' = alpha s + beta), for the raised threshold of the retry pass.
 __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* __restrict__ qf, int nq, int nq_pad,
                                                         int8_t* __restrict__ qa, double* __restrict__ delta,
+                                                        double* __restrict__ alpha, double* __restrict__ beta,
                                                         const double* __restrict__ bounds) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane_id();
   if (q >= nq_pad) return;
@@ -143,7 +145,11 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   if (q >= nq) {  // padding queries: zero pieces (their thresholds never accept)
     reinterpret_cast<int4*>(o)[l] = make_int4(0, 0, 0, 0);
     if (NPC == 2) reinterpret_cast<int4*>(o)[64 + l] = make_int4(0, 0, 0, 0);
-    if (l == 0) delta[q] = 0.0;
+    if (l == 0) {
+      delta[q] = 0.0;
+      alpha[q] = 0.0;
+      beta[q] = 0.0;
+    }
     return;
   }
   float qv[DPL];
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     while ((double)mx <= 127.0 * ldexp(1.0, e - 1)) --e;
   }
   const double invS = NPC == 2 ? ldexp(1.0, -e) : (mx > 0.f ? 127.0 / (double)mx : 1.0);
-  double r2 = 0.0, r1 = 0.0, q2 = 0.0, q1 = 0.0;
+  double r2 = 0.0, r1 = 0.0, q2 = 0.0, q1 = 0.0, qs = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const double x = (double)qv[i] * invS;  // exact for two pieces
@@ -176,6 +182,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     r1 += fabs(rho);
     q2 += (double)qv[i] * (double)qv[i];
     q1 += fabs((double)qv[i]);
+    qs += (double)qv[i];
     const int dim = DPL * l + i, s = dim >> 5;
     const int pos = s * 32 + (mode == VRQ_GEMM_BINARY ? ph2_pos(dim & 31) : (dim & 31));
     o[pos] = (int8_t)a;
@@ -185,6 +192,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   r1 = wave_sum_f64(r1);
   q2 = wave_sum_f64(q2);
   q1 = wave_sum_f64(q1);
+  qs = wave_sum_f64(qs);
   constexpr double SLACK = 1.0 / (1 << 20);  // >= 16 f32 ulps of every rounding on the u path
   if (l == 0) {
     double d;
@@ -200,6 +208,9 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
       d = sqrt(r2) * (1.0 + SLACK) + SLACK * sqrt(q2) * invS;
     }
     delta[q] = d;
+    // u units of a reference score s (s' = alpha s + beta): Phase II (s + sum q) / (2S), else s / S
+    alpha[q] = mode == VRQ_GEMM_BINARY ? 0.5 * invS : invS;
+    beta[q] = mode == VRQ_GEMM_BINARY ? 0.5 * invS * qs : 0.0;
   }
 }
 
@@ -211,7 +222,8 @@ template <int PH, bool DENSE>
 __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     const uint8_t* __restrict__ src, const double* __restrict__ norms, int64_t n, const int8_t* __restrict__ qa,
     int nq, const float* __restrict__ thr, uint32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
-    int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, float* __restrict__ dv, int64_t dv_stride) {
+    int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, float* __restrict__ dv, int64_t dv_stride,
+    const int32_t* __restrict__ qbflag) {
   constexpr bool P3 = PH == VRQ_GEMM_INT8_COSINE;
   // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
   // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
@@ -228,6 +240,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   const int L = xcd_logical(blockIdx.x, gridDim.x);
   const int chunk = L / nqb, qb = L - chunk * nqb;
   if (chunk >= nchunks) return;
+  if (qbflag && qbflag[qb] == 0) return;  // retry pass: only query blocks holding a retried query
   const int64_t row0 = (int64_t)chunk * chunk_stride;
   const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
   if (row0 >= row1) return;
@@ -544,10 +557,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
 __global__ __launch_bounds__(256) void gemm_select_kernel(const float* __restrict__ dv, int64_t dv_stride,
                                                           int64_t scr, int64_t sstride, int nsc, int64_t n, int k,
                                                           const double* __restrict__ delta, float* __restrict__ thr,
-                                                          int32_t* __restrict__ ccnt, int nchunks, int nq) {
+                                                          int32_t* __restrict__ ccnt, int nchunks, int nq,
+                                                          int32_t* __restrict__ qbflag, int nqb) {
   __shared__ uint32_t hist[2048];
   __shared__ uint32_t res[3];
   const int q = blockIdx.x, tid = threadIdx.x;
+  if (q == 0)
+    for (int i = tid; i < nqb; i += 256) qbflag[i] = 0;
   if (q >= nq) {
     if (tid == 0) thr[q] = __builtin_inff();
     return;
@@ -713,10 +729,18 @@ struct FinShared {
   int32_t misc[4];
 };
 
-// finish: the query's candidate lists -> exact scores -> running top-k -> first min(k, n).  A list
-// overflow (rows the main pass could not record) or fewer than min(k, n) candidates (zero-norm rows)
-// flags the query for the fallback instead.
-template <int PH>
+// finish: the query's candidate lists -> exact scores -> running top-k -> first min(k, n), with the
+// query's flag (fb_flag): 0 = served; 2 = retry; 1 = exact fallback.
+//   A list overflow (more rows passed the sampled threshold than a list holds: a query whose
+//   neighbourhood the sample under-represents) with >= min(k, n) recorded candidates -> RETRY: the
+//   k-th best exact score s_k among the recorded candidates is a lower bound of the true k-th score,
+//   so every row of the exact top-k (ties with the k-th included) has u >= alpha s_k + beta - Delta;
+//   that raised threshold goes to thr[q] and the query block to the retry main pass.
+//   Fewer than min(k, n) candidates (zero-norm rows) -> the fallback.
+// Pass 2 (RETRY = true) serves the retried queries from the retry pass's lists; an overflow there
+// goes to the fallback.  A served or abandoned query's thr becomes +inf, so a retry pass over its
+// query block records nothing for it.
+template <int PH, bool RETRY>
 __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t n,
                                                           int64_t row_offset, const float* __restrict__ qf, int k,
                                                           const uint32_t* __restrict__ cand,
@@ -724,9 +748,14 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
                                                           int32_t* __restrict__ out_count,
                                                           int64_t* __restrict__ out_rows,
                                                           double* __restrict__ out_scores,
-                                                          int32_t* __restrict__ fb_flag) {
+                                                          int32_t* __restrict__ fb_flag, float* __restrict__ thr,
+                                                          const double* __restrict__ alpha,
+                                                          const double* __restrict__ beta,
+                                                          const double* __restrict__ delta,
+                                                          int32_t* __restrict__ qbflag) {
   __shared__ FinShared sh;
   const int q = blockIdx.x, tid = threadIdx.x;
+  if (RETRY && fb_flag[q] != 2) return;
   if (tid == 0) sh.misc[1] = 0;  // overflow
   __syncthreads();
   const int32_t* cq = ccnt + (int64_t)q * nchunks;
@@ -746,10 +775,13 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   const int need = (int)((int64_t)k < n ? k : n);
 #ifdef VRQ_G5_DEBUG
   if (tid == 0 && (sh.misc[1] || total < need || q < 4))
-    printf("q %d candidates %d overflow %d capc %d\n", q, total, sh.misc[1], capc);
+    printf("q %d retry %d candidates %d overflow %d capc %d\n", q, (int)RETRY, total, sh.misc[1], capc);
 #endif
-  if (sh.misc[1] || total < need) {
-    if (tid == 0) fb_flag[q] = 1;
+  if (total < need || (RETRY && sh.misc[1])) {
+    if (tid == 0) {
+      fb_flag[q] = 1;
+      thr[q] = __builtin_inff();
+    }
     return;
   }
   const uint32_t* Cq = cand + (int64_t)q * nchunks * capc;
@@ -767,6 +799,16 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
   const int kc = running_topk<PH>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2]);
+  if (!RETRY && sh.misc[1]) {  // overflow: raise the threshold to the recorded k-th score, retry
+    if (tid == 0) {
+      const double sk = desc_key_inv(sh.key[kc - 1]);
+      const double t2 = alpha[q] * sk + beta[q] - delta[q];
+      thr[q] = __double2float_rd(t2 - 1e-9 * fabs(t2));
+      fb_flag[q] = 2;
+      atomicOr(&qbflag[q / GQB], 1);
+    }
+    return;
+  }
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)sh.row[i] + row_offset : -1;
@@ -775,6 +817,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   if (tid == 0) {
     out_count[q] = kc;
     fb_flag[q] = 0;
+    thr[q] = __builtin_inff();
   }
 }
 
@@ -791,7 +834,7 @@ __global__ __launch_bounds__(256) void gemm_fallback_kernel(const Rows c, int64_
   __shared__ uint32_t row[KMAX5 + FB_BATCH];
   __shared__ int32_t fill;
   const int q = blockIdx.x, tid = threadIdx.x;
-  if (!fb_flag[q]) return;
+  if (fb_flag[q] != 1) return;
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
   const int kc =
@@ -811,7 +854,7 @@ struct GemmPlan {
   int nsc;
   int64_t chunk_rows;
   int nchunks, capc;
-  size_t off_delta, off_thr, off_flag, off_cnt, off_cand, off_dv, bytes;
+  size_t off_delta, off_alpha, off_beta, off_qbf, off_thr, off_flag, off_cnt, off_cand, off_dv, bytes;
 };
 
 static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
@@ -847,11 +890,17 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   const int64_t expect = ((int64_t)k * cr + Sv - 1) / Sv;
   int capc = 64;
   while (capc < CAP_MULT * expect && capc < 4096) capc <<= 1;
+  // headroom for neighbourhoods stored contiguously (a cluster in one chunk): at least 512 entries
+  // per list while all lists of the batch stay within 1 GiB
+  while (capc < 512 && (double)nq * p->nchunks * (2 * capc) * sizeof(uint32_t) <= (double)(1 << 30)) capc <<= 1;
   p->capc = capc;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t qa = al((size_t)p->nq_pad * QA_BYTES);
   p->off_delta = qa;
-  p->off_thr = p->off_delta + al((size_t)p->nq_pad * sizeof(double));
+  p->off_alpha = p->off_delta + al((size_t)p->nq_pad * sizeof(double));
+  p->off_beta = p->off_alpha + al((size_t)p->nq_pad * sizeof(double));
+  p->off_qbf = p->off_beta + al((size_t)p->nq_pad * sizeof(double));
+  p->off_thr = p->off_qbf + al((size_t)p->nqb * sizeof(int32_t));
   p->off_flag = p->off_thr + al((size_t)p->nq_pad * sizeof(float));
   p->off_cnt = p->off_flag + al((size_t)nq * sizeof(int32_t));
   p->off_cand = p->off_cnt + al((size_t)nq * p->nchunks * sizeof(int32_t));
@@ -930,12 +979,23 @@ bool gemm_mode_ok(int mode) {
   return mode == VRQ_GEMM_BINARY || mode == VRQ_GEMM_INT8_COSINE || mode == VRQ_GEMM_FLOAT_IP;
 }
 
+// finish -> retry main pass (query blocks with a retried query) -> finish of the retried queries ->
+// exact fallback of the rest
 template <int PH>
-void launch_finish(const Rows& c, int64_t n, int64_t row_offset, const float* qf, int nq, int k, const GemmPlan& p,
-                   const uint32_t* cand, const int32_t* cnt, int32_t* out_count, int64_t* out_rows,
-                   double* out_scores, int32_t* flag, bool fb, hipStream_t s) {
-  hipLaunchKernelGGL(gemm_finish_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, cand, cnt,
-                     p.nchunks, p.capc, out_count, out_rows, out_scores, flag);
+void launch_finish(const Rows& c, const uint8_t* src, int64_t n, int64_t row_offset, const float* qf, int nq, int k,
+                   const GemmPlan& p, const int8_t* qa, float* thr, uint32_t* cand, int32_t* cnt, int32_t* out_count,
+                   int64_t* out_rows, double* out_scores, int32_t* flag, const double* alpha, const double* beta,
+                   const double* delta, int32_t* qbf, bool fb, hipStream_t s) {
+  constexpr int MP = PH == VRQ_GEMM_BINARY ? VRQ_GEMM_BINARY : VRQ_GEMM_INT8_COSINE;  // matrix-pass kind
+  hipLaunchKernelGGL((gemm_finish_kernel<PH, false>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
+                     (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
+                     flag, thr, alpha, beta, delta, qbf);
+  hipLaunchKernelGGL((gemm_topk_kernel<MP, false>), dim3(p.nchunks * p.nqb), dim3(GW * 64), 0, s, src, c.norms, n, qa,
+                     nq, (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
+                     (float*)nullptr, (int64_t)0, (const int32_t*)qbf);
+  hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
+                     (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
+                     flag, thr, alpha, beta, delta, qbf);
   if (fb)
     hipLaunchKernelGGL(gemm_fallback_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, out_count,
                        out_rows, out_scores, (const int32_t*)flag);
@@ -956,6 +1016,9 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
   uint8_t* ws = (uint8_t*)workspace;
   int8_t* qa = (int8_t*)ws;
   double* delta = (double*)(ws + p.off_delta);
+  double* alpha = (double*)(ws + p.off_alpha);
+  double* beta = (double*)(ws + p.off_beta);
+  int32_t* qbf = (int32_t*)(ws + p.off_qbf);
   float* thr = (float*)(ws + p.off_thr);
   int32_t* flag = (int32_t*)(ws + p.off_flag);
   int32_t* cnt = (int32_t*)(ws + p.off_cnt);
@@ -967,20 +1030,20 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
   const dim3 blk(GW * 64);
   if (st & VRQ_GEMM_STAGE_SAMPLE) {
     hipLaunchKernelGGL(gemm_prep_kernel, dim3((p.nq_pad + 3) / 4), dim3(256), 0, s, mode, qf, nq, p.nq_pad, qa,
-                       delta, bounds);
+                       delta, alpha, beta, bounds);
     VRQ_LAUNCH_CHECK();
     const dim3 grid(p.nsc * p.nqb);
     if (P3)
       hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, true>), grid, blk, 0, s, src, rn, n, qa, nq,
                          (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
-                         p.nqb, dv, p.scols);
+                         p.nqb, dv, p.scols, (const int32_t*)nullptr);
     else
       hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, true>), grid, blk, 0, s, src, rn, n, qa, nq,
                          (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
-                         p.nqb, dv, p.scols);
+                         p.nqb, dv, p.scols, (const int32_t*)nullptr);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, p.scr,
-                       p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq);
+                       p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq, qbf, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_GEMM_STAGE_MAIN) {
@@ -988,11 +1051,11 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
     if (P3)
       hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_INT8_COSINE, false>), grid, blk, 0, s, src, rn, n, qa, nq,
                          (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
-                         (float*)nullptr, (int64_t)0);
+                         (float*)nullptr, (int64_t)0, (const int32_t*)nullptr);
     else
       hipLaunchKernelGGL((gemm_topk_kernel<VRQ_GEMM_BINARY, false>), grid, blk, 0, s, src, rn, n, qa, nq,
                          (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
-                         (float*)nullptr, (int64_t)0);
+                         (float*)nullptr, (int64_t)0, (const int32_t*)nullptr);
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_GEMM_STAGE_FINISH) {
@@ -1000,15 +1063,17 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
     // queries' outputs unwritten, to prove the matrix-core path alone served a batch
     const char* fe = getenv("VRQ_GEMM_FALLBACK");
     const bool fb = !(fe && fe[0] == '0');
+    const int8_t* qac = qa;
+    const double *al = alpha, *be = beta, *de = delta;
     if (mode == VRQ_GEMM_INT8_COSINE)
-      launch_finish<VRQ_GEMM_INT8_COSINE>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows,
-                                          out_scores, flag, fb, s);
+      launch_finish<VRQ_GEMM_INT8_COSINE>(c, src, n, row_offset, qf, nq, k, p, qac, thr, cand, cnt, out_count,
+                                          out_rows, out_scores, flag, al, be, de, qbf, fb, s);
     else if (mode == VRQ_GEMM_FLOAT_IP)
-      launch_finish<VRQ_GEMM_FLOAT_IP>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows, out_scores,
-                                       flag, fb, s);
+      launch_finish<VRQ_GEMM_FLOAT_IP>(c, src, n, row_offset, qf, nq, k, p, qac, thr, cand, cnt, out_count, out_rows,
+                                       out_scores, flag, al, be, de, qbf, fb, s);
     else
-      launch_finish<VRQ_GEMM_BINARY>(c, n, row_offset, qf, nq, k, p, cand, cnt, out_count, out_rows, out_scores,
-                                     flag, fb, s);
+      launch_finish<VRQ_GEMM_BINARY>(c, src, n, row_offset, qf, nq, k, p, qac, thr, cand, cnt, out_count, out_rows,
+                                     out_scores, flag, al, be, de, qbf, fb, s);
     VRQ_LAUNCH_CHECK();
   }
   return VRQ_OK;

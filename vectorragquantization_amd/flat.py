@@ -161,6 +161,8 @@ class FloatIndexIDMap:
         r = rows.cpu().numpy()
         s = scores.cpu().numpy()
         ids = self.id_map.cpu().numpy()
+        if (cnt < 0).any():  # only when the VRQ_GEMM_FALLBACK=0 test hook skipped a query's fallback
+            raise N.VrqNativeError("FloatIndexIDMap.search: a query was left unserved (exact fallback disabled)")
         for j in range(nq):
             c = int(cnt[j])
             D[j, :c] = s[j, :c].astype(np.float32)
