@@ -55,8 +55,11 @@ def _near(rng, base, nflip):
 
 
 @pytest.mark.parametrize("n,nq,K", [(65_536, 1, 100), (70_001, 300, 100), (200_000, 130, 10),
-                                    (131_072, 257, 128), (100_003, 128, 1), (500_000, 520, 100)])
-def test_mfma_phase1_vs_faiss_restatement(dev, oracle_lib, n, nq, K):
+                                    (131_072, 257, 128), (100_003, 128, 1), (500_000, 520, 100),
+                                    # the row-split small-batch kernel K1r: MB = 1, 2, 4
+                                    (80_000, 20, 100), (90_017, 33, 100), (120_000, 64, 128), (150_001, 100, 50)])
+@pytest.mark.parametrize("scan", ["mfma", "valu"])
+def test_mfma_phase1_vs_faiss_restatement(dev, oracle_lib, n, nq, K, scan):
     rng = np.random.default_rng(n * 7 + nq + K)
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     src = rng.integers(0, n, nq)
@@ -64,14 +67,14 @@ def test_mfma_phase1_vs_faiss_restatement(dev, oracle_lib, n, nq, K):
     qb[0] = codes[n - 1]                                  # exact hit on the very last row
     codes[rng.integers(0, n, 64)] = qb[-1]                # duplicates of one query across the corpus
     D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
-    c, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
+    c, D1, I1 = _phase1(codes, qb, K, dev, scan)
     assert np.array_equal(c, np.full(nq, K))
     assert np.array_equal(D0, D1)
     assert np.array_equal(I0, I1)
 
 
 def test_mfma_auto_selection_in_hamming_topk(dev, oracle_lib):
-    """vrq_hamming_topk picks the matrix-core scan on its own for nq >= 128."""
+    """vrq_hamming_topk picks the matrix-core scan on its own (K <= 128, n >= 65536)."""
     from vectorragquantization_amd.index import BinaryIndexIDMap2
     rng = np.random.default_rng(5)
     n, nq = 150_000, 200
@@ -187,35 +190,38 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib):
 def _sample_rows(n, nq):
     """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S = n/32 rows
     clamped to [32768, 2^20], as 64-row tiles spread at a tile stride ts >= 64 over the corpus, in
-    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass)."""
+    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass; 1024 chunks for <= 64 queries)."""
     nqb = (nq + 255) // 256
     S = min(max(n // 32, 32768), 1 << 20) if n // 32 <= (1 << 20) else 1 << 20
     tiles = min(max(S // 64, 1), n // 64)
-    nsc = min(max(1, 256 // nqb), tiles)
+    # batches of <= 64 queries: the row-split kernel's sample pass, one chunk per wave (1024)
+    nsc = min(1024 if nq <= 64 else max(1, 256 // nqb), tiles)
     tiles = nsc * (tiles // nsc)
     ts = (n - 64) // (tiles - 1) if tiles > 1 else 64
     return (np.arange(tiles)[:, None] * ts + np.arange(64)[None, :]).reshape(-1)
 
 
-def test_mfma_sampled_threshold_rerun(dev, oracle_lib):
+@pytest.mark.parametrize("nq", [300, 100, 50])
+def test_mfma_sampled_threshold_rerun(dev, oracle_lib, nq):
     """The thresholded pass runs with the sampled tau_s = d_(j)+1 (j < K) of the dense sample.
-    Queries 0 and 290 (two different 256-query blocks) get 70 near copies (dist <= 20) on sample
+    Queries 0 and nq - 10 (two different 256-query blocks at nq = 300; the one block of the
+    row-split kernel at nq = 100) get 70 near copies (dist <= 20) on sample
     rows and 40 more at dist 30 off the sample, none elsewhere: d_(j) falls among the near
     copies, the dist-30 copies miss tau_s, the check finds C = 70 < K and the re-run with tau_p
     must recover the first 30 of them in row order.  The other queries take the fast path."""
     rng = np.random.default_rng(23)
-    n, nq, K = 100_000, 300, 100
+    n, K = 100_000, 100
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     qb = _near(rng, codes[rng.integers(0, n, nq)], 50)
     samp = _sample_rows(n, nq)
     off = np.setdiff1d(np.arange(n), samp)
-    for q in (0, 290):
+    for q in (0, nq - 10):
         near = rng.choice(samp, 70, replace=False)
         codes[near] = _near(rng, np.repeat(qb[q:q + 1], 70, axis=0), int(rng.integers(5, 21)))
         far = rng.choice(off, 40, replace=False)
         codes[far] = _near(rng, np.repeat(qb[q:q + 1], 40, axis=0), 30)
     D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
     _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
-    assert (D0[0] == 30).sum() == 30 and (D0[290] == 30).sum() == 30
+    assert (D0[0] == 30).sum() == 30 and (D0[nq - 10] == 30).sum() == 30
     assert np.array_equal(D0, D1)
     assert np.array_equal(I0, I1)

@@ -79,6 +79,7 @@ struct MfmaShape {
 };
 constexpr int kMbLarge = 4, kMbSmall = 2;
 constexpr int kMbLargeMinQueries = 512;     // batches of >= 512 queries take the MB = 4 kernel
+constexpr int kRowsMaxQueries = 128;        // batches of <= 128 queries take the row-split kernel K1r
 
 // 32 code bits -> one FP4 MFMA fragment lane: 32 e2m1 values.  Dword j, nibble i holds bit 4i + j
 // (a fixed permutation of k applied identically to queries and rows, so every dot product is
@@ -645,6 +646,307 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1r: the matrix-core scan for SMALL batches (nq <= 128): every wave streams its own rows.
+//
+// With few queries a row tile feeds few MFMAs, so sharing the unpacked tile between the four
+// waves of a workgroup (K1m) no longer pays for its barrier and LDS traffic: here each wave owns a
+// contiguous chunk of rows, LDS-DMAs its own packed tiles (ring of NPR per wave, no barrier), and
+// unpacks each 32-bit piece of a row straight into the B fragment registers of one k-step.  All MB
+// M-blocks (32 queries each, MB*32 >= nq) of the batch are in every wave.
+//   k-step s, lane (ri, h): dword 16h + s of row ri (so a lane reads its 64 contiguous bytes of
+//   the row: 4 conflict-free ds_read_b128 through the tile swizzle), queries the same dword.
+// Same thresholds (sampled tau_s / exact re-run with tau_p), same per-(query, chunk) lists and
+// suffix merge as K1m; the hit path flushes synchronously (hits are rare at the sizes this serves).
+constexpr int NPR = 3;  // per-wave packed ring depth (tile t+2 in flight while tile t is read)
+template <int MB>
+struct RowsShape {
+  static constexpr int QPW = 32 * MB;
+  static constexpr int SMEM = MWAVES * (NPR * PKT + QPW * 8 + (STG + 1) * 4 + MB * 128);
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
+
+template <int MODE, int MB>
+__global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
+    const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
+    const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
+    int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
+    const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
+  // DENSE = the sample pass (as K1m's): chunk c = this wave's T tiles, tile t at row
+  // c * chunk_stride + t * tile_stride (every tile whole), u16 distances to dv[q][c * chunk_rows + row]
+  constexpr bool DENSE = MODE == MFMA_SAMPLE;
+  constexpr int QPW = RowsShape<MB>::QPW;
+  if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
+  __shared__ __attribute__((aligned(16))) uint8_t smem[RowsShape<MB>::SMEM];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* pk = smem + w * (NPR * PKT);                                       // this wave's ring
+  int32_t* lcnt = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + w * QPW;
+  int32_t* tq = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + MWAVES * QPW + w * QPW;
+  int32_t* stg = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + 2 * MWAVES * QPW + w * (STG + 1);
+  float* sd = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + 2 * MWAVES * QPW +
+                                       MWAVES * (STG + 1)) + w * MB * 32;
+  const int l = lane_id();
+  const int h = l >> 5, ri = l & 31;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3, q8 = nb >> 3, r8 = nb & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int chunk = L * MWAVES + w;
+  if (chunk >= nchunks) return;
+  const int64_t row0 = (int64_t)chunk * chunk_stride;
+  const bool strided = tile_stride != RT;
+  const int64_t row1 = strided ? n : (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  if (row0 >= row1) return;
+  const int nrows = strided ? (int)chunk_rows : (int)(row1 - row0);
+  const int ntiles = (nrows + RT - 1) / RT;
+  const int nblk = 2 * ntiles;  // 32-row n-blocks
+
+  // LDS-DMA of packed tile t: 8 pieces of 64 x 16 B (the K1m swizzle), the last partial tile clamped
+  uint32_t doff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = i * 64 + l;
+    const int r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
+    doff[i] = (uint32_t)(r * 128 + c * 16);
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    uint8_t* buf = pk + (t % NPR) * PKT;
+    const int64_t tr0 = row0 + (int64_t)t * tile_stride;
+    if (tr0 + RT <= row1) {
+      const uint8_t* base = codes + tr0 * 128;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + i * 1024), 16,
+                                         0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        int64_t row = tr0 + (doff[i] >> 7);
+        row = row < row1 ? row : row1 - 1;
+        __builtin_amdgcn_global_load_lds(codes + row * 128 + (doff[i] & 127),
+                                         (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+      }
+    }
+  };
+  for (int t = 0; t < NPR && t < ntiles; ++t) issue(t);
+
+  // A fragments: k-step s, lane (ri, h) = dword 16h + s of query 32m + ri
+  v4i A[MB][KS];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int q = 32 * m + ri;
+    const bool qok = q < nq && (!rerun || rerun[q]);
+    const uint32_t* qp = reinterpret_cast<const uint32_t*>(queries + (int64_t)(qok ? q : 0) * 128);
+    int pc = 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint32_t wd = qok ? qp[16 * h + s] : 0u;
+      pc += __popc(wd);
+      A[m][s] = unpack_query32(wd);
+    }
+    pc += __shfl_xor(pc, 32, 64);  // both halves of the query
+    if (h == 0) tq[q] = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;
+  }
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(A[m][s]));
+  for (int i = l; i < QPW; i += 64) lcnt[i] = 0;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+    if (l < 32) {
+      const int g = l & 15, hh = l >> 4;
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
+    }
+  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), tq0 = lds_addr(tq), stg0 = lds_addr(stg);
+  const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
+  auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
+    v4i p0, p1, p2, p3;
+    lds_read128(p0, sd0 + (uint32_t)(m * 128));
+    lds_read128(p1, sd0 + (uint32_t)(m * 128 + 16));
+    lds_read128(p2, sd0 + (uint32_t)(m * 128 + 32));
+    lds_read128(p3, sd0 + (uint32_t)(m * 128 + 48));
+    const v16i x = __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                           __builtin_shufflevector(p2, p3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4,
+                                           5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    a = __builtin_bit_cast(v16f, x);
+  };
+  v16f acc[2][MB];
+  if constexpr (!DENSE)
+    static_for<0, MB>([&](auto M) {
+      constexpr int m = decltype(M)::value;
+      load_seed(acc[0][m], m);
+      load_seed(acc[1][m], m);
+    });
+  // this lane's 64 bytes of row (32 * (blk & 1) + ri) of the packed tile in ring slot `sl`
+  auto read_rows = [&](v4i (&d)[4], int blk) __attribute__((always_inline)) {
+    const int r = 32 * (blk & 1) + ri;
+    const uint32_t base = pk0 + (uint32_t)(((blk >> 1) % NPR) * PKT);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds_read128(d[i], base + (uint32_t)(pk_slot(r, 4 * h + i) * 16));
+  };
+  // at most k tiles' DMA still in flight
+  auto wait_tiles = [&](int k) __attribute__((always_inline)) {
+    if (k <= 0) wait_vm<0>();
+    else if (k == 1) wait_vm<8>();
+    else wait_vm<16>();
+  };
+  static_assert(NPR - 1 <= 2, "wait_tiles covers up to 2 tiles in flight");
+  wait_tiles((ntiles < NPR ? ntiles : NPR) - 1);  // tile 0 landed
+  v4i cur[4], nxt[4];
+  read_rows(cur, 0);
+  wait_lgkm0();
+
+  const int64_t qstride = (int64_t)nchunks * capc;
+  uint64_t* const cbase = cand + (int64_t)chunk * capc;  // + q * qstride + pos
+  int nst = 0;
+  auto flush_all = [&](int64_t base_row) __attribute__((always_inline)) {  // staged hits -> lists (sync)
+    if (nst > STG) {
+      for (int i = l; i < QPW; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
+      nst = STG;
+    }
+    for (int i0 = 0; i0 < nst; i0 += 64) {
+      const int i = i0 + l;
+      int e = 0, pos = 0;
+      if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+      const int ql = (e >> ENT_Q_SHIFT) & 127;
+      if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+      if (i < nst && pos < capc)
+        cbase[(int64_t)ql * qstride + pos] =
+            ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) | (uint64_t)(base_row + (e & 127));
+    }
+    nst = 0;
+  };
+  auto block_hits = [&](const v16f& a, int m, int pc, float hp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const uint64_t mask = __ballot(a[g] > hp);
+      if (mask) {
+        if ((mask >> l) & 1) {
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+          int lo = l;
+          asm volatile("" : "+v"(lo));
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+          int tql;
+          lds_read32(tql, tq0 + (uint32_t)(ql * 4));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tql)::"memory");
+          const int v = pc - (int)(2.0f * a[g]) + tql;
+          const int pos = nst + below < STG ? nst + below : STG;
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (lo & 31));
+        }
+        nst += __popcll(mask);
+      }
+    }
+  };
+
+  // DENSE: the 16 distances of M-block m of an n-block -> dv (local row lr of the chunk)
+  auto block_dense = [&](const v16f& a, int m, int pc, int lr) __attribute__((always_inline)) {
+    const int64_t col = (int64_t)chunk * chunk_rows + lr;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int q = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (q < nq) dv[(int64_t)q * dv_stride + col] = (uint16_t)(pc - (int)(2.0f * a[g]) + 1024);
+    }
+  };
+  // ---- main loop over n-blocks; k-step s runs the MB MFMAs of n-block blk on the unpacked dword
+  // s of `cur`, while the previous n-block's epilogue, this block's row popcount and the next
+  // block's packed reads fill the MFMA gaps ----
+  int pcs = 0;       // running row popcount of this n-block (this lane's half)
+  int pprev = 0;     // the previous n-block's row popcount (whole row)
+  int hpb = 0x7fffffff;
+  uint64_t hitm = 0;
+  auto nblock = [&](auto PAR, int blk) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;  // blk & 1 (n-blocks run in pairs: static accumulator indices)
+    // the next n-block's tile: its DMA landed (tile boundary), and the ring slot of tile t+NPR-1 ...
+    if (par == 1 && blk + 1 < nblk) {
+      const int t1 = (blk + 1) >> 1;  // tile about to be read
+      const int last = t1 + NPR - 2 < ntiles ? t1 + NPR - 2 : ntiles - 1;  // last tile issued so far
+      wait_tiles(last - t1);
+    }
+    const int lr = blk * 32 + ri;
+    static_for<0, KS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      const uint32_t wd = (uint32_t)cur[s >> 2][s & 3];
+      const v4i bfrag = unpack_row32(wd);
+      static_for<0, MB>([&](auto M) {
+        constexpr int m = decltype(M)::value;
+        if constexpr (s == 0 && !DENSE) asm volatile("" : "+v"(acc[par][m]));
+        acc[par][m] = mfma_fp4(A[m][s], bfrag, (s == 0 && DENSE) ? v16f{} : acc[par][m]);
+        asm volatile("" : "+v"(acc[par][m]));
+      });
+      VRQ_SCHED_FENCE();
+      if constexpr (s == 0)
+        pcs = __popc(wd);
+      else
+        pcs += __popc(wd);
+      // epilogue of the previous n-block: tests (s = 1 .. MB), branch (s = MB + 1), re-seeds
+      if constexpr (DENSE && s >= 1 && s < 1 + MB) {
+        if (blk > 0) block_dense(acc[par ^ 1][s - 1], s - 1, pprev, lr - 32);
+      }
+      if constexpr (!DENSE && s >= 1 && s < 1 + MB) {
+        constexpr int m = s - 1;
+        const v16i bb = __builtin_bit_cast(v16i, acc[par ^ 1][m]);
+        const int x0 = max(max(bb[0], bb[1]), bb[2]), x1 = max(max(bb[3], bb[4]), bb[5]);
+        const int x2 = max(max(bb[6], bb[7]), bb[8]), x3 = max(max(bb[9], bb[10]), bb[11]);
+        const int x4 = max(max(bb[12], bb[13]), bb[14]);
+        hitm |= __ballot(max(max(max(x0, x1), x2), max(max(x3, x4), bb[15])) > hpb);
+      }
+      if constexpr (!DENSE && s == MB + 1) {
+        if (hitm) {  // rare
+          const int lrp = lr - 32;
+          const int pc = lrp < nrows && blk > 0 ? pprev : 0x40000000;
+          const float hp = 0.5f * (float)pc;
+          static_for<0, MB>([&](auto M) {
+            constexpr int mm = decltype(M)::value;
+            if (any_above(acc[par ^ 1][mm], hp)) block_hits(acc[par ^ 1][mm], mm, pc, hp);
+          });
+          if (nst) flush_all(row0 + (int64_t)(blk - 1) * 32);
+        }
+        hitm = 0;
+      }
+      if constexpr (!DENSE && s >= MB + 2 && s < 2 * MB + 2) load_seed(acc[par ^ 1][s - MB - 2], s - MB - 2);
+      // the next n-block's packed data
+      if constexpr (s == 8)
+        if (blk + 1 < nblk) read_rows(nxt, blk + 1);
+      VRQ_SCHED_FENCE();
+    });
+    // row popcount of this n-block (both halves) and its threshold for the next n-block's tests
+    pprev = pcs + __shfl_xor(pcs, 32, 64);
+    hpb = __float_as_int(0.5f * (float)(lr < nrows ? pprev : 0x40000000));
+    // a tile consumed: refill its ring slot (the DMA of tile t + NPR)
+    if (par == 1 && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3])::"memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+  };
+  for (int blk = 0; blk < nblk; blk += 2) {  // nblk is even
+    nblock(std::integral_constant<int, 0>{}, blk);
+    nblock(std::integral_constant<int, 1>{}, blk + 1);
+  }
+  // epilogue of the last n-block (odd parity)
+  {
+    constexpr int par = 1;
+    const int lr = (nblk - 1) * 32 + ri;
+    if constexpr (DENSE) {
+      static_for<0, MB>([&](auto M) { block_dense(acc[par][decltype(M)::value], decltype(M)::value, pprev, lr); });
+    } else {
+      const int pc = lr < nrows ? pprev : 0x40000000;
+      const float hp = 0.5f * (float)pc;
+      static_for<0, MB>([&](auto M) {
+        constexpr int mm = decltype(M)::value;
+        if (any_above(acc[par][mm], hp)) block_hits(acc[par][mm], mm, pc, hp);
+      });
+      if (nst) flush_all(row0 + (int64_t)(nblk - 1) * 32);
+    }
+  }
+  wait_lgkm0();
+  if (!DENSE)
+    for (int i = l; i < QPW; i += 64)
+      if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
+}
+
 // Thresholds from the dense sample (S rows spread over the corpus, every distance exact):
 //   tau_p(q) = d_(K) + 1, accept dist <= the K-th smallest sample distance: the sample rows alone
 //              put >= K corpus rows under it, so the candidates always hold the exact top-K
@@ -961,6 +1263,15 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->mb = em && (atoi(em) == 2 || atoi(em) == 4) ? atoi(em) : nq >= kMbLargeMinQueries ? kMbLarge : kMbSmall;
   p->qpb = p->mb == kMbLarge ? MfmaShape<kMbLarge>::QPB : MfmaShape<kMbSmall>::QPB;
   p->nqb = (nq + p->qpb - 1) / p->qpb;
+  // small batches (nq <= 128): the row-split kernel K1r, all queries in every wave
+  // (VRQ_MFMA_ROWS=0/1: tuning override, read per call)
+  const char* er = getenv("VRQ_MFMA_ROWS");
+  p->rows = nq <= kRowsMaxQueries && !(er && er[0] == '0');
+  if (p->rows) {
+    p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
+    p->qpb = kRowsMaxQueries;
+    p->nqb = 1;
+  }
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
   // sample: S rows in 64-row tiles spread evenly over the corpus at a tile stride ts >= 64 (a sample
@@ -975,7 +1286,10 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   if (S < kMfmaMinSample) S = kMfmaMinSample;
   int64_t tiles = S / RT > 0 ? S / RT : 1;
   if (tiles > n / RT) tiles = n / RT;  // non-overlapping whole tiles (n >= kMfmaMinRows)
-  int64_t nsc = 256 / p->nqb_s;
+  // K1r with MB <= 2 runs the sample pass too (one sample chunk per wave); its MB = 4 instance would
+  // spill in the dense epilogue, so batches of 65..128 queries take K1m's (MB = 2) sample pass
+  p->rows_sample = p->rows && p->mb <= 2;
+  int64_t nsc = p->rows_sample ? 256 * MWAVES : 256 / p->nqb_s;
   if (nsc < 1) nsc = 1;
   if (nsc > tiles) nsc = tiles;
   const int64_t T = tiles / nsc;
@@ -987,8 +1301,8 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->sample_tile_stride = ts;
   p->sample = tiles * RT;  // dv columns = sample rows
   S = p->sample;
-  // thresholded pass over all n rows
-  int64_t want = 256 / p->nqb;
+  // thresholded pass over all n rows (K1r: one chunk per wave, 1024 waves)
+  int64_t want = p->rows ? 256 * MWAVES : 256 / p->nqb;
   if (want < 1) want = 1;
   int64_t cr = (n + want - 1) / want;
   cr = (cr + RT - 1) / RT * RT;
@@ -1016,7 +1330,7 @@ bool mfma_use(int64_t n, int nq, int K, int flags) {
   if (flags & VRQ_SEARCH_SCAN_VALU) return false;
   const bool ok = K <= kMfmaMaxK && n >= kMfmaMinRows;
   if (flags & VRQ_SEARCH_SCAN_MFMA) return ok;
-  return ok && nq >= kMfmaMinQueries;
+  return ok && nq >= kMfmaMinQueries;  // K1r serves even one query faster than the wavefront scan
 }
 
 int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
@@ -1044,7 +1358,29 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
       hipLaunchKernelGGL(kern2, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
                          crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
   };
-  if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
+  // K1r launches: the MB = 1 / 2 / 4 instance, one workgroup per 4 chunks
+  auto rows_pass = [&](auto k1, auto k2, auto k4, const int32_t* tau, const int32_t* rr, const int32_t* qf,
+                       int nch, int64_t crows, int64_t cstride, int64_t tstride, uint16_t* d, int64_t dstride) {
+    const dim3 g((unsigned)((nch + MWAVES - 1) / MWAVES)), blk(MWAVES * 64);
+    if (p.mb == 1)
+      hipLaunchKernelGGL(k1, g, blk, 0, s, codes, n, q, nq, tau, cand, ccnt, p.capc, crows, cstride, tstride, nch, rr,
+                         qf, d, dstride);
+    else if (p.mb == 2)
+      hipLaunchKernelGGL(k2, g, blk, 0, s, codes, n, q, nq, tau, cand, ccnt, p.capc, crows, cstride, tstride, nch, rr,
+                         qf, d, dstride);
+    else
+      hipLaunchKernelGGL(k4, g, blk, 0, s, codes, n, q, nq, tau, cand, ccnt, p.capc, crows, cstride, tstride, nch, rr,
+                         qf, d, dstride);
+  };
+  if ((st & VRQ_SCAN_STAGE_PREFIX) && p.rows_sample) {  // dense sample pass (K1r) + per-query thresholds
+    rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>,
+              hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
+              p.sample_stride, p.sample_tile_stride, dv, p.sample);
+    VRQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
+                       tau_s, tau_p, qbflag, p.nqb);
+    VRQ_LAUNCH_CHECK();
+  } else if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
     hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
                        0, s, codes, n, (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0,
                        p.sample_chunk_rows, p.sample_stride, p.sample_tile_stride, p.sample_chunks, p.nqb_s, none,
@@ -1054,7 +1390,12 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                        tau_s, tau_p, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
-  if (st & VRQ_SCAN_STAGE_MATRIX) {
+  if ((st & VRQ_SCAN_STAGE_MATRIX) && p.rows) {
+    rows_pass(hamming_mfma_rows_kernel<MFMA_MAIN, 1>, hamming_mfma_rows_kernel<MFMA_MAIN, 2>,
+              hamming_mfma_rows_kernel<MFMA_MAIN, 4>, (const int32_t*)(sampled ? tau_s : tau_p), none, none,
+              p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr, (int64_t)0);
+    VRQ_LAUNCH_CHECK();
+  } else if (st & VRQ_SCAN_STAGE_MATRIX) {
     pass(hamming_mfma_kernel<MFMA_MAIN, kMbLarge>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
          (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
          (uint16_t*)nullptr, (int64_t)0);
@@ -1065,9 +1406,15 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
     hipLaunchKernelGGL(sample_check_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, (const int32_t*)ccnt, p.nchunks, K,
                        nq, rerun, qbflag, p.qpb);
     VRQ_LAUNCH_CHECK();
-    pass(hamming_mfma_kernel<MFMA_RERUN, kMbLarge>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
-         (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
-         (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);
+    if (p.rows)
+      rows_pass(hamming_mfma_rows_kernel<MFMA_RERUN, 1>, hamming_mfma_rows_kernel<MFMA_RERUN, 2>,
+                hamming_mfma_rows_kernel<MFMA_RERUN, 4>, (const int32_t*)tau_p, (const int32_t*)rerun,
+                (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
+                (int64_t)0);
+    else
+      pass(hamming_mfma_kernel<MFMA_RERUN, kMbLarge>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
+           (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
+           (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_SCAN_STAGE_SUFFIX) {  // candidates of the whole corpus -> one sorted K-list per query

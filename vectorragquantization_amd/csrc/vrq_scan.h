@@ -35,7 +35,7 @@ constexpr int kMfmaMaxK = 128;           // K bound of the path
 constexpr int64_t kMfmaMinSample = 32768;
 constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~1.3 ms at nq = 1024)
 constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
-constexpr int kMfmaMinQueries = 128;     // auto-selection threshold on the batch size
+constexpr int kMfmaMinQueries = 1;       // auto-selection threshold on the batch size (K1r below 129)
 constexpr int64_t kMfmaSampleDiv = 32;   // dense threshold sample = n / kMfmaSampleDiv rows
 
 struct MfmaPlan {
@@ -46,7 +46,9 @@ struct MfmaPlan {
   int sample_chunks;
   int j;                     // sampled threshold order (tau_s = d_(j) + 1); K = tau_p only
   int capc;                  // candidate capacity per (query, chunk) list
-  int mb;                    // M-blocks (32 queries) per wave of the matrix kernel: 4 or 2
+  int rows;                  // 1: the row-split small-batch kernel K1r (nq <= 128, nqb = 1)
+  int rows_sample;           // 1: K1r also runs the dense sample pass (nq <= 64)
+  int mb;                    // M-blocks (32 queries) per wave of the matrix kernel: 4 or 2 (K1r: 1, 2, 4)
   int qpb;                   // queries per workgroup (128 * mb)
   int nqb;                   // query blocks of the thresholded pass
   int nqb_s;                 // query blocks of the dense sample pass (always the MB = 2 kernel)
