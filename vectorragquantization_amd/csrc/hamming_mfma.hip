@@ -970,8 +970,10 @@ __global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __re
   if (tid < 32) atomicAdd(&pcq, __popc(reinterpret_cast<const uint32_t*>(queries + (int64_t)qi * 128)[tid]));
   const uint16_t* d = dv + (int64_t)qi * S;
   const int64_t S8 = S & ~int64_t(7);
-  for (int64_t i = (int64_t)tid * 8; i < S8; i += 256 * 8) {  // 16-B loads: 8 values
-    const uint4 w = *reinterpret_cast<const uint4*>(d + i);
+  // 16-B loads of 8 values, 8 loads in flight per thread (one workgroup per query: with few queries
+  // the pass is latency-bound on a handful of CUs)
+  constexpr int U = 8;
+  auto add8 = [&](const uint4& w) {
     const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -979,7 +981,16 @@ __global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __re
       if (lo < NB) atomicAdd(&hist[lo], 1u);
       if (hi < NB) atomicAdd(&hist[hi], 1u);
     }
+  };
+  int64_t i = (int64_t)tid * 8;
+  for (; i + (U - 1) * 256 * 8 < S8; i += U * 256 * 8) {
+    uint4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = *reinterpret_cast<const uint4*>(d + i + u * 256 * 8);
+#pragma unroll
+    for (int u = 0; u < U; ++u) add8(w[u]);
   }
+  for (; i < S8; i += 256 * 8) add8(*reinterpret_cast<const uint4*>(d + i));
   for (int64_t i = S8 + tid; i < S; i += 256)
     if (d[i] < NB) atomicAdd(&hist[d[i]], 1u);
   __syncthreads();
