@@ -528,3 +528,13 @@ class QuantVectorDB:
             out.append((e, float(dequant_scores(np.asarray(qv, np.float32).reshape(1, -1), row)[0, 0])))
         out.sort(key=lambda h: h[1], reverse=True)
         return out[:k]
+
+
+def rerank_results(cand_ids, cand_docs, results):
+    """``CohereVectorDBInt8.search_rerank_cohere``'s last step (``CohereVectorDBInt8.py:329-338``):
+    each rerank result's ``index`` points into the candidate list; ``score`` = ``relevance_score``;
+    Python's stable sort by score descending over the service's result order."""
+    out = [{"doc_id": cand_ids[r["index"]], "score": r["relevance_score"], "doc": cand_docs[r["index"]]}
+           for r in results]
+    out.sort(key=lambda x: x["score"], reverse=True)
+    return out

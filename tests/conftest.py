@@ -58,3 +58,9 @@ def golden_vdb():
 def golden_vdb_real():
     import numpy as np
     return dict(np.load(os.path.join(GOLDEN, "vectordb_real.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_cohere_int8():
+    import numpy as np
+    return dict(np.load(os.path.join(GOLDEN, "cohere_int8.npz")))

@@ -43,7 +43,11 @@ payload.
   -- the last one Snappy-compressed), so tests can open reference folders with the product's
   RocksDict reader on a box where /root/reference does not exist.
 
-Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real|flat_real|ref_db ...]
+* ``CohereVectorDBInt8`` ``add_documents`` / ``search`` / ``search_rerank_cohere`` with the Cohere
+  embed and rerank services replaced by tests/golden/fake_services.py -> ``cohere_int8.npz``.
+
+Usage:  python tests/golden/make_golden.py [encoders|dequant|search_synth|search_real|flat_real|
+        vectordb_synth|vectordb_real|cohere_int8|ref_db ...]
 """
 from __future__ import annotations
 
@@ -649,6 +653,119 @@ def gen_vectordb_real(out_path: str):
     print("wrote", out_path)
 
 
+# ---------------------------------------------------------------------------
+# 5. CohereVectorDBInt8: Hamming-only search + search_rerank_cohere (fake Cohere services)
+# ---------------------------------------------------------------------------
+COHERE_INT8_SEARCHES = {"k10": (10, 10), "k5": (5, 3), "k30": (30, 2)}
+
+
+def _ref_cohere_int8(table, folder="/nonexistent", config=None):
+    from tests.golden.fake_services import FakeCohereRequests
+    mod = _import_ref("CohereVectorDBInt8")
+    fake = FakeCohereRequests(table)
+    mod.requests = fake
+    db = object.__new__(mod.CohereVectorDBInt8)    # skip __init__ (env vars, Rdict, folders)
+    db.embedding_dim = 1024
+    db.endpoint = "https://embed.invalid/v2/embed"
+    db.api_key = "embed-key"
+    db.folder = folder
+    db.config = dict(config or {"version": "1.0", "model": "embed-english-v3.0", "embedding_dim": 1024})
+    db.index = O.IndexBinaryIDMap2(1024)
+    db.doc_db = {}
+    db.save = lambda: None
+    return db, fake
+
+
+def _cohere_int8_searches(db, fake, queries, table, out, prefix):
+    os.environ["COHERE_RERANK_ENDPOINT"] = "https://rerank.invalid"
+    os.environ["COHERE_RERANK_KEY"] = "rerank-key"
+    nq = queries.shape[0]
+    for j in range(nq):
+        table[f"{prefix}q{j}"] = queries[j]
+    for cname, (k, osb) in COHERE_INT8_SEARCHES.items():
+        for kind in ("search", "rerank"):
+            ids = np.full((nq, k), -1, np.int64)
+            sc = np.full((nq, k), np.nan)
+            cnt = np.zeros(nq, np.int64)
+            sent = np.full((nq, k * osb), -1, np.int64)      # doc ids of the rerank request, in order
+            for j in range(nq):
+                qt = f"{prefix}q{j}"
+                if kind == "search":
+                    r = db.search(qt, k=k, binary_oversample=osb)
+                else:
+                    fake.calls.clear()
+                    r = db.search_rerank_cohere(qt, k=k, binary_oversample=osb)
+                    url, hdr, payload = fake.calls[-1]
+                    assert url == "https://rerank.invalid/v2/rerank" and payload["top_n"] == k
+                    assert payload["model"] == "rerank-english-v3.0" and payload["query"] == qt
+                    assert hdr["Authorization"] == "Bearer rerank-key"
+                    # the request's documents are texts; map them back through Phase I's ids
+                    _, d_ids = db.index.search(np.packbits(table[qt] > np.mean(table[qt])).reshape(1, -1),
+                                               min(k * osb, db.index.ntotal))
+                    keep = [int(e) for e in d_ids[0] if e != -1 and "doc" in db.doc_db.get(str(int(e)), {})]
+                    assert [db.doc_db[str(e)]["doc"] for e in keep] == payload["documents"]
+                    sent[j, :len(keep)] = keep
+                cnt[j] = len(r)
+                for i, h in enumerate(r):
+                    ids[j, i] = h["doc_id"]
+                    sc[j, i] = h["score"]
+            key = f"{prefix}{kind}_{cname}"
+            out.update({f"{key}_ids": ids, f"{key}_score": sc, f"{key}_cnt": cnt})
+            if kind == "rerank":
+                out[f"{key}_sent"] = sent
+
+
+def gen_cohere_int8(out_path: str):
+    """``CohereVectorDBInt8.add_documents`` / ``remove_document`` / ``search`` /
+    ``search_rerank_cohere`` (``CohereVectorDBInt8.py:137-339``) with the Cohere services replaced by
+    tests/golden/fake_services.py: (1) a synthetic int8 corpus (clustered floats x 1270, planted
+    duplicate rows, two removals, a re-add and one id added twice); (2) the reference's persisted
+    ``db_cohere_int8`` folder (index.bin + RocksDict SST, read with the product's reader), queries =
+    stored int8 rows plus noise."""
+    from vectorragquantization_amd.docstore import RocksDictReader
+    rng = np.random.default_rng(8181)
+    N = 600
+    X8 = np.clip(np.round(synth_corpus(rng, N, nclusters=20) * 1270.0), -128, 127).astype(np.int8)
+    for a, b in ((3, 300), (4, 301), (4, 302)):
+        X8[b] = X8[a]
+    texts = [f"t{i}" for i in range(N)]
+    ids = (np.arange(N, dtype=np.int64) * 3 + 7).tolist()
+    nq = 16
+    src = rng.integers(0, N, nq)
+    src[0], src[1] = 3, 4
+    Q8 = np.clip(X8[src].astype(np.int64) + rng.integers(-6, 7, (nq, 1024)), -128, 127).astype(np.int8)
+    Q8[0] = X8[3]
+    res = {"X8": X8, "ids": np.array(ids), "Q8": Q8}
+    table = {t: X8[i] for i, t in enumerate(texts)}
+    db, fake = _ref_cohere_int8(table)
+    db.add_documents(ids, texts, batch_size=64, save=False)
+    db.remove_document(ids[10], save=False)
+    db.remove_document(ids[11], save=False)
+    db.add_documents([ids[11], 9001, 9001], ["t12", "t5", "t6"], save=False)
+    res["id_map"] = db.index.id_map.copy()
+    res["codes"] = db.index.xb.copy()
+    _cohere_int8_searches(db, fake, Q8, table, res, "")
+    # the persisted reference folder
+    import json as _json
+    folder = os.path.join(REF, "db_cohere_int8")
+    store = RocksDictReader(os.path.join(folder, "docs"))
+    R8 = np.stack([np.asarray(store[str(i)]["int8"], np.int8) for i in range(1000)])
+    rq = 12
+    rsrc = rng.integers(0, 1000, rq)
+    RQ8 = np.clip(R8[rsrc].astype(np.int64) + rng.integers(-10, 11, (rq, 1024)), -128, 127).astype(np.int8)
+    res["real_Q8"] = RQ8
+    table = {}
+    db, fake = _ref_cohere_int8(table, folder, _json.load(open(os.path.join(folder, "config.json"))))
+    xb, idm = read_ibm2(os.path.join(folder, "index.bin"))
+    db.index.add_with_ids(xb, idm)
+    for key, val in store.items():
+        db.doc_db[key] = val
+    res["real_ntotal"] = np.int64(db.index.ntotal)
+    _cohere_int8_searches(db, fake, RQ8, table, res, "real_")
+    np.savez_compressed(out_path, **res)
+    print("wrote", out_path)
+
+
 def gen_ref_db(out_dir: str):
     """Byte copies of persisted reference data files (no source): the folders tests open."""
     import shutil
@@ -656,7 +773,7 @@ def gen_ref_db(out_dir: str):
              "db_cohere_enhanced/docs/CURRENT", "db_cohere_float/config.json", "db_cohere_float/docs/000009.sst",
              "db_cohere_float/docs/CURRENT", "db_int4_global/config.json", "db_int4_global/index.bin",
              "db_int4_global/docs/000009.sst", "db_int4_global/docs/CURRENT"]
-    for folder in ("db_int8_global", "db_int16_global", "db_int8", "db_int4", "db_int16"):
+    for folder in ("db_int8_global", "db_int16_global", "db_int8", "db_int4", "db_int16", "db_cohere_int8"):
         files += [f"{folder}/config.json", f"{folder}/index.bin", f"{folder}/docs/000009.sst", f"{folder}/docs/CURRENT"]
     for f in files:
         dst = os.path.join(out_dir, f)
@@ -684,5 +801,7 @@ if __name__ == "__main__":
         gen_vectordb_synth(os.path.join(HERE, "vectordb_synth.npz"))
     if not only or "vectordb_real" in only:
         gen_vectordb_real(os.path.join(HERE, "vectordb_real.npz"))
+    if not only or "cohere_int8" in only:
+        gen_cohere_int8(os.path.join(HERE, "cohere_int8.npz"))
     if not only or "ref_db" in only:
         gen_ref_db(os.path.join(HERE, "ref_db"))

@@ -9,10 +9,10 @@ from ._native import VrqNativeError, load as load_native  # noqa: F401
 
 __all__ = ["VrqNativeError", "load_native", "CohereEnhancedVectorDB", "BinaryIndexIDMap2", "encode",
            "ShardedSearch", "CohereVectorDBFloat", "VectorDBInt8Global", "VectorDBInt16Global", "VectorDBInt4Global",
-           "VectorDBInt8", "VectorDBInt4", "VectorDBInt16"]
+           "VectorDBInt8", "VectorDBInt4", "VectorDBInt16", "CohereVectorDBInt8"]
 
 _VECTORDB = ("VectorDBInt8Global", "VectorDBInt16Global", "VectorDBInt4Global", "VectorDBInt8", "VectorDBInt4",
-             "VectorDBInt16")
+             "VectorDBInt16", "CohereVectorDBInt8")
 
 
 def __getattr__(name):  # lazy: importing the package must not require a GPU

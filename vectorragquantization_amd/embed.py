@@ -11,6 +11,10 @@ one POST of ``{"model", "texts", "embedding_bits": 16}`` for the whole batch.
 Both return ``{text: vector}`` like the reference; quantisation happens on the
 GPU for the whole batch (``vrq_encode``).
 
+``CohereInt8HTTPProvider`` is ``CohereVectorDBInt8._generate_int8_embeddings`` (int8 only) and
+``CohereRerankHTTPProvider`` the ``/v2/rerank`` call of ``search_rerank_cohere``
+(``CohereVectorDBInt8.py:237-339``), both used by ``vectordb.CohereVectorDBInt8``.
+
 ``CohereHTTPProvider`` reproduces ``CohereEnhancedVectorDB._get_embeddings``
 (``CohereEnhancedVectorDB.py:136-169``): one JSON POST to ``/v2/embed`` with
 ``model``, ``texts``, ``input_type``, ``truncate: NONE``, ``embedding_types``;
@@ -58,6 +62,79 @@ class CohereHTTPProvider:
         except Exception as e:  # same contract as the reference: log + {}
             logger.error("Embedding generation failed: %s", str(e))
             return {}
+
+
+class CohereInt8HTTPProvider(CohereHTTPProvider):
+    """``CohereVectorDBInt8._generate_int8_embeddings`` (``CohereVectorDBInt8.py:84-128``): one POST of
+    the batch asking for ``embedding_types: ["int8"]``; each text's vector is
+    ``embeddings.int8[i]`` (squeezed), texts of the wrong dimension skipped with a log line."""
+
+    def __init__(self, endpoint: str | None = None, api_key: str | None = None, model: str = "embed-english-v3.0",
+                 embedding_dim: int = 1024):
+        super().__init__(endpoint, api_key, model)
+        self.dim = embedding_dim
+
+    def embed_int8(self, texts, input_type: str = "search_document") -> dict:
+        emb = self.embed(texts, input_type, ["int8"])
+        out = {}
+        if not emb:
+            return out
+        for i, text in enumerate(texts):
+            try:
+                a = np.array(emb["int8"][i], dtype=np.int8)
+                if a.ndim > 1:
+                    a = a[0]
+                if a.shape[0] != self.dim:
+                    logger.error(f"Embedding dimension mismatch for text='{text}'. "
+                                 f"Got {a.shape[0]}, expected {self.dim}. Skipping.")
+                    continue
+                out[text] = a
+            except Exception as ex:   # the reference logs and skips the text
+                logger.error(f"Error processing int8 embedding for text='{text}': {ex}")
+        return out
+
+
+class CohereRerankHTTPProvider:
+    """The Cohere ``/v2/rerank`` call of ``CohereVectorDBInt8.search_rerank_cohere``
+    (``CohereVectorDBInt8.py:256-326``).  Endpoint and key come from ``COHERE_RERANK_ENDPOINT`` /
+    ``COHERE_RERANK_KEY`` when not given; ``/v2/rerank`` is appended unless the endpoint already ends
+    with it.  ``rerank`` POSTs ``{"model", "query", "top_n", "documents"}`` with a Bearer key and
+    returns the response's ``results`` list (``[{"index", "relevance_score"}, ...]``), or ``None``
+    after logging when the call fails or the response has no results -- the reference then
+    returns ``[]``."""
+
+    def __init__(self, endpoint: str | None = None, api_key: str | None = None):
+        self.endpoint = endpoint if endpoint is not None else os.environ.get("COHERE_RERANK_ENDPOINT")
+        if self.endpoint and not self.endpoint.endswith("/v2/rerank"):
+            self.endpoint = self.endpoint.rstrip("/") + "/v2/rerank"
+        self.api_key = api_key if api_key is not None else os.environ.get("COHERE_RERANK_KEY")
+
+    def configured(self) -> bool:
+        if not self.endpoint:
+            logger.error("COHERE_RERANK_ENDPOINT not set in the environment.")
+            return False
+        if not self.api_key:
+            logger.error("COHERE_RERANK_KEY not set in the environment.")
+            return False
+        return True
+
+    def rerank(self, query: str, documents, top_n: int, model: str = "rerank-english-v3.0"):
+        import requests
+        headers = {"Authorization": f"Bearer {self.api_key}", "Content-Type": "application/json"}
+        payload = {"model": model, "query": query, "top_n": top_n, "documents": list(documents)}
+        logger.info("Calling Cohere rerank API at %s", self.endpoint)
+        try:
+            r = requests.post(self.endpoint, headers=headers, json=payload)
+            r.raise_for_status()
+            data = r.json()
+        except Exception as e:
+            logger.error("Rerank API call failed: %s", str(e))
+            return None
+        results = data.get("results")
+        if not results:
+            logger.error("Rerank response missing 'results'.")
+            return None
+        return results
 
 
 class OllamaHTTPProvider:
@@ -133,6 +210,9 @@ class TableProvider:
 
     def embed_int16(self, texts) -> dict:
         return {t: np.asarray(self.table[t], dtype=np.int16) for t in texts if t in self.table}
+
+    def embed_int8(self, texts, input_type: str = "search_document") -> dict:
+        return {t: np.asarray(self.table[t], dtype=np.int8) for t in texts if t in self.table}
 
 
 def text_seed(text: str) -> int:

@@ -37,7 +37,10 @@ def _device(device=None) -> torch.device:
 def as_device_tensor(x, dtype, device) -> torch.Tensor:
     if isinstance(x, torch.Tensor):
         return x.to(device=device, dtype=dtype).contiguous()
-    return torch.from_numpy(np.ascontiguousarray(np.asarray(x), dtype=torch_to_np(dtype))).to(device)
+    a = np.ascontiguousarray(np.asarray(x), dtype=torch_to_np(dtype))
+    if not a.flags.writeable:      # read-only (e.g. np.load) arrays: torch.from_numpy needs a writable buffer
+        a = a.copy()
+    return torch.from_numpy(a).to(device)
 
 
 def torch_to_np(dtype):

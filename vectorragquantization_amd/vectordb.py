@@ -64,7 +64,8 @@ class _QuantizedVectorDB:
     QDTYPE = torch.int8
     LOCAL = False           # per-row (min, max)
     GLOBAL = False          # config.json carries global_limit
-    HAMMING_ONLY = False    # VectorDBInt16
+    HAMMING_ONLY = False    # VectorDBInt16, CohereVectorDBInt8
+    VEC_DTYPE = torch.float32   # embeddings as the provider returns them
     EMPTY_MSG = "If you want to create a new database, the folder must be empty."
 
     def __init__(self, folder: str, model: str, embedding_dim: int, global_limit, rdict_options, embed_url: str,
@@ -228,16 +229,22 @@ class _QuantizedVectorDB:
         return int(doc_id) in self.texts
 
     # -- documents ---------------------------------------------------------------------
-    def _embed(self, texts) -> dict:
+    def _embed(self, texts, input_type: str = "search_document") -> dict:
         return self.provider.embed_int16(texts) if self.HAMMING_ONLY else self.provider.embed_floats(texts)
+
+    def _codes(self, X):
+        """ubinary codes (+ quantised rows) of a device batch in one ``vrq_encode`` launch; the
+        integer classes threshold at the float64 mean, exact for int8 as for int16 rows."""
+        if self.HAMMING_ONLY and X.dtype != torch.int16:
+            X = X.to(torch.int16)
+        return Q.encode(self.MODE, X, self.limit if self.GLOBAL else 1.0, self.device)
 
     def add_vectors(self, doc_ids, X, docs=None, save: bool = False) -> None:
         """Append embeddings (f32[m, d]; i16[m, d] for VectorDBInt16) without HTTP: one ``vrq_encode``
         launch computes the ubinary codes and the quantised rows of the whole batch."""
         ids = np.asarray(doc_ids.cpu() if isinstance(doc_ids, torch.Tensor) else doc_ids, dtype=np.int64).reshape(-1)
-        dt = torch.int16 if self.HAMMING_ONLY else torch.float32
-        X = as_device_tensor(X, dt, self.device).reshape(ids.shape[0], self.embedding_dim)
-        e = Q.encode(self.MODE, X, self.limit if self.GLOBAL else 1.0, self.device)
+        X = as_device_tensor(X, self.VEC_DTYPE, self.device).reshape(ids.shape[0], self.embedding_dim)
+        e = self._codes(X)
         self.index.add_with_ids(e["codes"], ids)
         if not self.HAMMING_ONLY:
             self._q.append(e["q"])
@@ -302,9 +309,8 @@ class _QuantizedVectorDB:
         n = self.index.ntotal
         if k < 0 or binary_oversample < 0:
             raise ValueError("k and binary_oversample must be non-negative")
-        dt = torch.int16 if self.HAMMING_ONLY else torch.float32
-        qv = as_device_tensor(query, dt, self.device).reshape(-1, self.embedding_dim)
-        qb = Q.encode(self.MODE, qv, self.limit if self.GLOBAL else 1.0, self.device)["codes"]
+        qv = as_device_tensor(query, self.VEC_DTYPE, self.device).reshape(-1, self.embedding_dim)
+        qb = self._codes(qv)["codes"]
         with torch.cuda.device(self.device):
             if self.HAMMING_ONLY:
                 rows, ham, sc = Q.vectordb_search("bin16", self.index.codes, None, None, qb, k, binary_oversample)
@@ -334,7 +340,7 @@ class _QuantizedVectorDB:
         if self.index.ntotal == 0:
             logger.error("No documents indexed. Please add documents before searching.")
             return []
-        emb = self._embed([query])
+        emb = self._embed([query], "search_query")
         if not emb or query not in emb:
             logger.error("Query embedding generation failed. Returning empty results.")
             return []
@@ -405,7 +411,7 @@ class VectorDBInt4(_QuantizedVectorDB, Q.VectorDBInt4):
 class VectorDBInt16(_QuantizedVectorDB, Q.VectorDBInt16):
     """``VectorDBInt16.py:16``: int16 embeddings from the service thresholded to 1 bit/dimension;
     Hamming-only search."""
-    MODE, QKEY, QDTYPE, HAMMING_ONLY = "bin16", "int16", torch.int16, True
+    MODE, QKEY, QDTYPE, HAMMING_ONLY, VEC_DTYPE = "bin16", "int16", torch.int16, True, torch.int16
     EMPTY_MSG = "To create a new database, the folder must be empty."
 
     def __init__(self, folder: str, model: str = "snowflake-arctic-embed2", embedding_dim: int = 1024,
@@ -417,6 +423,66 @@ class VectorDBInt16(_QuantizedVectorDB, Q.VectorDBInt16):
         if self.config.get("model") != model or self.config.get("embedding_dim") != embedding_dim:   # :71-76
             logger.warning("Config model/dim differs from constructor arguments. "
                            f"config={self.config}, constructor=(model={model}, dim={embedding_dim})")
+
+
+class CohereVectorDBInt8(_QuantizedVectorDB):
+    """``CohereVectorDBInt8.py:11``: Cohere int8 embeddings only, ``packbits(int8 > mean)`` codes
+    (``:130-135``; the float64 mean of int8 rows is exact, so the ``bin16`` encode of the rows widened
+    to int16 is bit-identical), Hamming-only ``search`` (``:192-235``: ``score`` = the distance) and
+    ``search_rerank_cohere`` (``:237-339``): the Phase-I candidates of the gfx950 scan handed to the
+    Cohere ``/v2/rerank`` service.  ``provider`` replaces the ``COHERE_EMBED_*`` HTTP client
+    (``CohereInt8HTTPProvider``, which raises like the reference's constructor when the variables are
+    unset); ``rerank_provider`` the ``COHERE_RERANK_*`` one (read per call, as the reference does)."""
+    MODE, QKEY, QDTYPE, HAMMING_ONLY, VEC_DTYPE = "bin16", "int8", torch.int8, True, torch.int8
+    EMPTY_MSG = "To create a new database, the folder must be empty."
+
+    def __init__(self, folder: str, model: str = "embed-english-v3.0", embedding_dim: int = 1024,
+                 rdict_options=None, *, provider=None, rerank_provider=None, device=None):
+        if provider is None:
+            from .embed import CohereInt8HTTPProvider
+            provider = CohereInt8HTTPProvider(model=model, embedding_dim=embedding_dim)
+        self.rerank_provider = rerank_provider
+        super().__init__(folder, model, embedding_dim, None, rdict_options, None, provider, device)
+        if getattr(provider, "model", None) is not None and "model" in self.config:
+            provider.model = self.config["model"]     # the request posts self.config["model"] (:95)
+
+    def _embed(self, texts, input_type: str = "search_document") -> dict:
+        return self.provider.embed_int8(texts, input_type)
+
+    def search_rerank_cohere(self, query: str, k: int = 10, binary_oversample: int = 10,
+                             rerank_model: str = "rerank-english-v3.0") -> List[Dict]:
+        """Phase I over the whole index (``binary_k = min(k * binary_oversample, ntotal)`` candidates
+        in FAISS order, ``:281-285``), their texts (``:288-295``), one rerank request with
+        ``top_n = k`` (``:307-312``) and the results mapped back through ``index`` and stably sorted
+        by ``relevance_score`` descending (``:329-338``).  Every failure logs and returns ``[]``."""
+        from .embed import CohereRerankHTTPProvider
+        rr = self.rerank_provider if self.rerank_provider is not None else CohereRerankHTTPProvider()
+        if not rr.configured():
+            return []
+        if self.index.ntotal == 0:
+            logger.error("No documents indexed. Please add documents before searching.")
+            return []
+        emb = self._embed([query], "search_query")
+        if not emb or query not in emb:
+            logger.error("Query embedding generation failed. Returning empty results.")
+            return []
+        binary_k = min(k * binary_oversample, self.index.ntotal)
+        hits = self.search_vectors(emb[query], binary_k, 1)[0][0].cpu().numpy().tolist() if binary_k > 0 else []
+        cand_ids, cands = [], []
+        for e in hits:
+            if e != -1 and e in self.texts:
+                cand_ids.append(int(e))
+                cands.append(self.texts[e])
+        if not cands:
+            logger.error("No candidate documents found for reranking.")
+            return []
+        results = rr.rerank(query, cands, k, rerank_model)
+        if not results:
+            return []
+        out = [{"doc_id": cand_ids[r["index"]], "score": r["relevance_score"], "doc": cands[r["index"]]}
+               for r in results]
+        out.sort(key=lambda x: x["score"], reverse=True)
+        return out
 
 
 def find_closest(db, query: str) -> Dict:
