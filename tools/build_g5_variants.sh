@@ -14,7 +14,7 @@ done
 wait
 for spec in "$@"; do
   name=${spec%%=*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJ/hamming_scan.o $OBJ/hamming_mfma.o $OBJ/select_rescore.o \
-    $OBJ/encode.o tools/probes/g5/gemm_$name.o -o tools/probes/g5/lib_$name.so
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $(ls $OBJ/*.o | grep -v gemm_topk.o) \
+    tools/probes/g5/gemm_$name.o -o tools/probes/g5/lib_$name.so
   echo tools/probes/g5/lib_$name.so
 done

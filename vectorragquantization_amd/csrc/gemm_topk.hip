@@ -14,12 +14,14 @@
 //     s' the reference score in the same units (Phase III: s/S; Phase II: (s + sum q)/(2S)):
 //       Phase III  Delta = ||rho||_2 (Cauchy-Schwarz; the score divides by ||x||_2) + f32 slack
 //       Phase II   Delta = ||rho||_1 (x in {0,1})                                  + f32 slack
-//  2. sample pass (dense): u for every (query, row) of an evenly spread row sample into dv, where
+//  2. sample pass (dense): u for every (query, row) of an evenly spread row sample, where
 //     u = fl(A_0 [+ A_1/256]) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
-//     (x = the int8 row, or the code's bits expanded to 0/1 bytes).
-//  3. select: U = the k-th largest sample u of the query, thr = U - 2 Delta (rounded down).  k sample
-//     rows have s' >= U - Delta, so every row of the exact top-k -- ties with the k-th included --
-//     has u >= thr.
+//     (x = the int8 row, or the code's bits expanded to 0/1 bytes).  Only the running max of u per
+//     (query, sample chunk, lane row) leaves the kernel: 32 values per query and chunk, each the u
+//     of a distinct sample row (the [nq, S] matrix is never written).
+//  3. select: U = the k-th largest of those maxima (<= the k-th largest sample u), thr = U - 2 Delta
+//     (rounded down).  k distinct sample rows have u >= U, so s' >= U - Delta, and every row of the
+//     exact top-k -- ties with the k-th included -- has u >= thr.
 //  4. main pass: every row with u >= thr is appended to a per-(query, chunk) candidate list.
 //  5. finish: exact reference scores of the candidates, running top-k by (s desc, row asc).  A list
 //     overflow (heavy ties) or fewer than min(k, n) candidates (zero-norm rows) sends the query to
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   float ures[NE];
   float umax = -__builtin_inff();
 #pragma unroll
-  for (int e = 0; e < NE; ++e) ures[e] = 0.f;
+  for (int e = 0; e < NE; ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
   float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
@@ -392,13 +394,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   auto flush = [&](int tt) {
     const int lr = tstart(tt) + r;
     const bool ok = lane_valid(tt);
-    if constexpr (DENSE) {
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int q = qbase + qrow(e);
-        if (q < nq && ok) dv[(int64_t)q * dv_stride + (int64_t)chunk * chunk_rows + lr] = ures[e];
-      }
-    } else {
+    if constexpr (!DENSE) {
       if (__ballot(umax >= 0.f)) {  // rare: ~k * n / sample rows per query over the corpus
         uint32_t m = 0;
         static_for<0, NE>([&](auto E) {
@@ -419,10 +415,15 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       umax = -__builtin_inff();
     }
   };
-  auto test = [&](float u, int e) {
-    ures[e] = u;
-    if constexpr (!DENSE) {  // pairs fold into one v_max3
-      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));
+  // the sample pass keeps, per (lane, test), the running max of u over the chunk's rows of that
+  // lane (NaN: none yet; rows already seen in the previous tile, and Phase-III zero norms, are NaN
+  // and drop out of the max); vp = this lane's row of the tested tile is new
+  auto test = [&](float u, int e, bool vp) {
+    if constexpr (DENSE) {
+      ures[e] = fmaxf(ures[e], vp ? u : __builtin_nanf(""));
+    } else {
+      ures[e] = u;
+      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));  // pairs fold into one v_max3
     }
   };
 
@@ -454,7 +455,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         wait_vm<0>();
     }
     if (!(VRQ_G5_BISECT & 4)) barrier_all();
-    if (t >= 2) flush(t - 2);
+    if (!DENSE && t >= 2) flush(t - 2);
+    const bool vprev = DENSE ? lane_valid(t - 1) : true;  // (the sample pass's test of tile t-1)
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
     const bool dma = t + AHEAD < ntiles;
     const DmaTile dt = dma_tile(dma ? t + AHEAD : t, sl == 0 ? NP - 1 : sl - 1);
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       constexpr int EOFF = NE == 16 ? 4 : 0;
       if constexpr (s >= EOFF && s < EOFF + NE) {
         constexpr int e = s - EOFF;
-        if constexpr (!first && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e);
+        if constexpr (!first && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e, vprev);
       }
       if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
         invc = (nv > 0.0 && lane_valid(t)) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
@@ -538,12 +540,21 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   if (t < ntiles) tile(I1{}, NOTFIRST{}, t);
   wait_vm<0>();
   // tile ntiles-2 (tested during the last tile), then the last tile itself
-  if (ntiles >= 2) flush(ntiles - 2);
+  if (!DENSE && ntiles >= 2) flush(ntiles - 2);
   const int pl = (ntiles - 1) & 1;
+  const bool vlast = lane_valid(ntiles - 1);
 #pragma unroll
   for (int e = 0; e < NE; ++e)
-    test(pl ? uval(acc[1][0], acc[1][1], e, invp) : uval(acc[0][0], acc[0][1], e, invp), e);
-  flush(ntiles - 1);
+    test(pl ? uval(acc[1][0], acc[1][1], e, invp) : uval(acc[0][0], acc[0][1], e, invp), e, vlast);
+  if constexpr (DENSE) {  // the lane maxima of the chunk -> dv[q][chunk * 32 + r]
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int q = qbase + qrow(e);
+      if (q < nq) dv[(int64_t)q * dv_stride + (int64_t)chunk * GRT + r] = ures[e];
+    }
+  } else {
+    flush(ntiles - 1);
+  }
   if constexpr (!DENSE) {
     wait_lgkm0();
     if (l < GQW && qbase + l < nq) ccnt[(int64_t)(qbase + l) * nchunks + chunk] = lcnt[w * GQW + l];
@@ -551,7 +562,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// select: per query, U = k-th largest valid sample u (3-pass radix select on the monotone key),
+// select: per query, U = k-th largest valid value of dv (the sample pass's lane maxima: nsc chunks of
+// scr = 32 values; 3-pass radix select on the monotone key),
 // thr = U - 2 Delta rounded down (-inf when the sample holds fewer than k finite values); zeroes the
 // query's list lengths for the main pass.  Padding queries get thr = +inf.
 __global__ __launch_bounds__(256) void gemm_select_kernel(const float* __restrict__ dv, int64_t dv_stride,
@@ -880,7 +892,7 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   p->scr = scr;
   p->nsc = (int)nsc;
   p->sstride = n / nsc >= scr ? n / nsc : scr;  // chunks never overlap; the last may be cut at n
-  p->scols = nsc * scr;
+  p->scols = nsc * GRT;  // dv columns per query: one running max per (sample chunk, lane row)
   int64_t cr = (n + want - 1) / want;
   cr = (cr + GRT - 1) / GRT * GRT;
   if ((n + cr - 1) / cr > MAX_CHUNKS) cr = ((n + MAX_CHUNKS - 1) / MAX_CHUNKS + GRT - 1) / GRT * GRT;
@@ -1042,7 +1054,7 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
                          (const float*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr, 0, p.scr, p.sstride, p.nsc,
                          p.nqb, dv, p.scols, (const int32_t*)nullptr);
     VRQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, p.scr,
+    hipLaunchKernelGGL(gemm_select_kernel, dim3(p.nq_pad), dim3(256), 0, s, (const float*)dv, p.scols, (int64_t)GRT,
                        p.sstride, p.nsc, n, k, (const double*)delta, thr, cnt, p.nchunks, nq, qbf, p.nqb);
     VRQ_LAUNCH_CHECK();
   }

@@ -130,10 +130,11 @@ __device__ __forceinline__ bool any_above(const v16f& a, float thr) {
   return __ballot(max(y0, y1) > __float_as_int(thr)) != 0;
 }
 
-// Staged hit entry (u32): (v + 1024) << 14 | query-in-wave << 7 | row - (t-1)*64, where
-// v = dist - pc(q) in [-1024, 1024] and the row is relative to the previous tile's first row
-// (the epilogue of a tile's second n-block runs in the next tile's iteration).
-constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7;
+// Staged hit entry (u32): (v + 1025) << 14 | query-in-wave << 7 | row - (t-1)*64, where
+// v = dist - tau(q) in [-1025, -1] (tau = the threshold the pass ran with; the suffix kernel adds it
+// back) and the row is relative to the previous tile's first row (the epilogue of a tile's second
+// n-block runs in the next tile's iteration).  List keys carry the same field: (v + 1025) << 40 | row.
+constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7, ENT_V_BIAS = 1025;
 
 // DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) is written
 // as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + local row].  Chunk c
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
   };
   const uint32_t pk0 = lds_addr(pk), ub0 = lds_addr(ub), pcr0 = lds_addr(pcr);
-  const uint32_t lc0 = lds_addr(lcnt), tq0 = lds_addr(tq), stg0 = lds_addr(stg);
+  const uint32_t lc0 = lds_addr(lcnt), stg0 = lds_addr(stg);
   // unit u of this wave = (nblk, piece) = ((4w+u) >> 3, (4w+u) & 7): lane -> tile row
   // 32*nblk + ri; piece p (dwords 4p..4p+3) holds k-steps 2p, 2p+1; lane-half h takes dword
   // 4p+2h of step 2p and 4p+2h+1 of step 2p+1 (one 8-byte read per lane).  Unpacked layout
@@ -395,12 +396,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           int lo = l;
           asm volatile("" : "+v"(lo));
           const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
-          int tql;  // tau'(q): acc = <q,r> + tau'/2
-          lds_read32(tql, tq0 + (uint32_t)(ql * 4));
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tql)::"memory");
-          const int v = pc - (int)(2.0f * a[g]) + tql;  // dist - pc(q): exact integers
+          // acc = <q,r> + tau'/2 with tau' = tau(q) - pc(q), so pc(r) - 2 acc = dist - tau(q) in
+          // [-1025, -1] for a hit (exact integers): no per-query value to fetch on this path
+          const int v = pc - (int)(2.0f * a[g]);
           const int pos = nst + below < STG ? nst + below : STG;
-          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
         }
         nst += __popcll(mask);
       }
@@ -757,7 +757,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
       const int g = l & 15, hh = l >> 4;
       sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
     }
-  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), tq0 = lds_addr(tq), stg0 = lds_addr(stg);
+  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), stg0 = lds_addr(stg);
   const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
   auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
     v4i p0, p1, p2, p3;
@@ -829,12 +829,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
           int lo = l;
           asm volatile("" : "+v"(lo));
           const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
-          int tql;
-          lds_read32(tql, tq0 + (uint32_t)(ql * 4));
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tql)::"memory");
-          const int v = pc - (int)(2.0f * a[g]) + tql;
+          const int v = pc - (int)(2.0f * a[g]);  // dist - tau(q), as in K1m
           const int pos = nst + below < STG ? nst + below : STG;
-          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + 1024) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (lo & 31));
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (lo & 31));
         }
         nst += __popcll(mask);
       }
@@ -957,7 +954,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
 __global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __restrict__ dv, int64_t S,
                                                             const uint8_t* __restrict__ queries, int K, int j,
                                                             int32_t* __restrict__ tau_s, int32_t* __restrict__ tau_p,
-                                                            int32_t* __restrict__ qbflag, int nqb) {
+                                                            int32_t* __restrict__ rerun, int32_t* __restrict__ qbflag,
+                                                            int nqb) {
   constexpr int NB = 2049;
   __shared__ uint32_t hist[NB + 3];
   __shared__ int pcq;
@@ -1027,6 +1025,7 @@ __global__ __launch_bounds__(256) void sample_select_kernel(const uint16_t* __re
       const int dj = rj < NB ? rj - 1024 + pcq : 1024;
       tau_p[qi] = dk + 1;
       tau_s[qi] = (j < K ? dj : dk) + 1;
+      rerun[qi] = 0;  // (the suffix reads tau_p for re-run queries; until a recheck, none)
     }
   }
 }
@@ -1051,8 +1050,8 @@ __global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __rest
 }
 
 // Suffix candidates -> one sorted list of K keys per query (KEY_NONE padded).
-// The matrix-core kernel left, per (query, chunk), a list of keys (v + 1024) << 40 | row and its
-// length.  Exact in every case:
+// The matrix-core kernel left, per (query, chunk), a list of keys (v + 1025) << 40 | row
+// (v = dist - tau(q)) and its length.  Exact in every case:
 //   all lists complete, total <= SUF_CAP  -> sort them all;
 //   all lists complete, total  > SUF_CAP  -> histogram of v, threshold T = K-th smallest v, sort
 //                                            the keys with v <= T (if they fit);
@@ -1160,7 +1159,10 @@ __global__ __launch_bounds__(SUF_THREADS) void suffix_topk_kernel(const uint8_t*
                                                                    const uint8_t* __restrict__ queries,
                                                                    const uint64_t* __restrict__ cand,
                                                                    const int32_t* __restrict__ ccnt, int nchunks,
-                                                                   int capc, int K, uint64_t* __restrict__ out) {
+                                                                   int capc, int K, const int32_t* __restrict__ tau_main,
+                                                                   const int32_t* __restrict__ tau_p,
+                                                                   const int32_t* __restrict__ rerun,
+                                                                   uint64_t* __restrict__ out) {
   __shared__ SufShared sh;
   const int qi = blockIdx.x, tid = threadIdx.x;
   if (tid < 32) sh.qw[tid] = reinterpret_cast<const uint32_t*>(queries + (int64_t)qi * 128)[tid];
@@ -1183,8 +1185,10 @@ __global__ __launch_bounds__(SUF_THREADS) void suffix_topk_kernel(const uint8_t*
   int total;
   int off = suf_excl_scan(mine, &total, sh.scan);
   const bool overflow = __syncthreads_or(over) != 0;
-  const int pcq = sh.misc[4];
-  const int64_t dfix = (int64_t)pcq - 1024;  // dist = v-field + pc(q) - 1024
+  // the threshold the query's lists were recorded with: the main pass's, or tau_p after a re-run;
+  // dist = v-field + tau(q) - ENT_V_BIAS
+  const int tauq = (rerun && rerun[qi]) ? tau_p[qi] : tau_main[qi];
+  const int64_t dfix = (int64_t)tauq - ENT_V_BIAS;
   int m = -1;
   bool real_dist = false;
   if (!overflow && total <= SUF_CAP) {
@@ -1389,7 +1393,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
               p.sample_stride, p.sample_tile_stride, dv, p.sample);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
-                       tau_s, tau_p, qbflag, p.nqb);
+                       tau_s, tau_p, rerun, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   } else if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
     hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
@@ -1398,7 +1402,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                        none, dv, p.sample);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
-                       tau_s, tau_p, qbflag, p.nqb);
+                       tau_s, tau_p, rerun, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_MATRIX) && p.rows) {
@@ -1430,7 +1434,8 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   }
   if (st & VRQ_SCAN_STAGE_SUFFIX) {  // candidates of the whole corpus -> one sorted K-list per query
     hipLaunchKernelGGL(suffix_topk_kernel, dim3(nq), dim3(SUF_THREADS), 0, s, codes, n, (int64_t)0, q, cand, ccnt,
-                       p.nchunks, p.capc, K, suffix);
+                       p.nchunks, p.capc, K, (const int32_t*)(sampled ? tau_s : tau_p), (const int32_t*)tau_p,
+                       (const int32_t*)(sampled ? rerun : nullptr), suffix);
     VRQ_LAUNCH_CHECK();
   }
   return VRQ_OK;
