@@ -21,6 +21,7 @@ ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--env", action="append", default=[])
 ap.add_argument("--modes", default="2,3")
+ap.add_argument("--stages", default="16,32,64", help="stage flags to time (64 = finish; bisect builds: skip it)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 sh = synth.make_corpus(a.n, device=dev)
@@ -28,6 +29,7 @@ qf, _, _ = synth.make_queries(a.n, a.nq, device=dev)
 libs = [p for p in os.environ.get("VRQ_LIBS", "").split(",") if p] or [None]
 envs = a.env or [""]
 modes = [int(m) for m in a.modes.split(",")]
+stages = [int(x) for x in a.stages.split(",")]
 ref = None
 import ctypes as C  # noqa: E402
 from vectorragquantization_amd import _native as N  # noqa: E402
@@ -51,9 +53,9 @@ for path in libs:
             cnt = torch.empty((a.nq,), dtype=torch.int32, device=dev)
             rows = torch.empty((a.nq, a.k), dtype=torch.int64, device=dev)
             sc = torch.empty((a.nq, a.k), dtype=torch.float64, device=dev)
-            times = {16: [], 32: [], 64: []}
+            times = {st_: [] for st_ in stages}
             for it in range(a.iters + 1):
-                for stage in (16, 32, 64):
+                for stage in stages:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     rc = lib.vrq_gemm_topk(mode, N.ptr(sh["codes"]), N.ptr(sh["x8"]), N.ptr(sh["norms"]), a.n, 1024,

@@ -9,7 +9,7 @@ OUT=gpurun_out/${TAG:-sweep}
 mkdir -p $OUT
 if [ -n "${G5_ENVS+x}" ]; then
   EARGS=""; for e in ${G5_ENVS}; do EARGS="$EARGS --env $e"; done
-  VRQ_LIBS=${G5_LIBS:-} timeout -k 10 ${G5_T:-500} python -u tools/gemm_probe.py --n ${G5_N:-10000000} --iters 3 $EARGS > $OUT/g5.jsonl 2> $OUT/g5.err || { echo G5_FAIL; tail -20 $OUT/g5.err; exit 1; }
+  VRQ_LIBS=${G5_LIBS:-} timeout -k 10 ${G5_T:-500} python -u tools/gemm_probe.py --n ${G5_N:-10000000} --iters 3 ${G5_ARGS:-} $EARGS > $OUT/g5.jsonl 2> $OUT/g5.err || { echo G5_FAIL; tail -20 $OUT/g5.err; exit 1; }
   cat $OUT/g5.jsonl
 fi
 for e in ${C2_ENVS:-}; do

@@ -26,6 +26,8 @@ for f in glob.glob("$OUT/pmc_p*/**/*counter_collection.csv", recursive=True):
         if "hamming_mfma_kernel<0>" in n or "gemm_topk_kernel" in n or "hamming_scan" in n:
             key = n.split("(")[0][-40:]
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+                agg[key]["dur_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
 for k, d in agg.items():
     print(k, {c: round(sum(v) / len(v)) for c, v in sorted(d.items())})
 PY

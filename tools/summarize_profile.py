@@ -21,7 +21,10 @@ def short(name):
     if "gemm_topk_kernel" in name:  # <PH, DENSE>: PH 3 = int8 cosine, 2 = binary
         t = name.split("gemm_topk_kernel<", 1)[-1]
         base = "gemm_topk_kernel" if t.startswith("3") else "gemm_topk_kernel_binary"
-        return base + ("_sample" if "true" in t.split(">")[0] else "")
+        targs = [x.strip() for x in t.split(">")[0].split(",")]  # PH, DENSE[, RETRY]
+        if len(targs) > 2 and targs[2] == "true":
+            return base + "_retry"
+        return base + ("_sample" if targs[1:2] == ["true"] else "")
     for nm in ("gemm_select_kernel", "gemm_finish_kernel", "gemm_fallback_kernel", "gemm_prep_kernel"):
         if nm in name:
             return nm + ("_binary" if "<2>" in name else "")

@@ -220,7 +220,9 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
 // The matrix pass.  PH = VRQ_GEMM_BINARY / VRQ_GEMM_INT8_COSINE; DENSE = the sample pass (u of
 // every (query, row) -> dv[q][chunk * chunk_rows + row]) else the thresholded pass (u >= thr[q] ->
 // candidate lists).  Chunk c covers rows [c * chunk_stride, + chunk_rows).
-template <int PH, bool DENSE>
+// RETRY: the retry pass of launch_finish (same code; a separate symbol so kernel traces and counter
+// summaries keep the main pass's per-launch figures apart from the retry's near-empty launch).
+template <int PH, bool DENSE, bool RETRY = false>
 __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     const uint8_t* __restrict__ src, const double* __restrict__ norms, int64_t n, const int8_t* __restrict__ qa,
     int nq, const float* __restrict__ thr, uint32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
@@ -1002,7 +1004,7 @@ void launch_finish(const Rows& c, const uint8_t* src, int64_t n, int64_t row_off
   hipLaunchKernelGGL((gemm_finish_kernel<PH, false>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
                      (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
                      flag, thr, alpha, beta, delta, qbf);
-  hipLaunchKernelGGL((gemm_topk_kernel<MP, false>), dim3(p.nchunks * p.nqb), dim3(GW * 64), 0, s, src, c.norms, n, qa,
+  hipLaunchKernelGGL((gemm_topk_kernel<MP, false, true>), dim3(p.nchunks * p.nqb), dim3(GW * 64), 0, s, src, c.norms, n, qa,
                      nq, (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
                      (float*)nullptr, (int64_t)0, (const int32_t*)qbf);
   hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,

@@ -136,8 +136,8 @@ __device__ __forceinline__ bool any_above(const v16f& a, float thr) {
 // n-block runs in the next tile's iteration).  List keys carry the same field: (v + 1025) << 40 | row.
 constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7, ENT_V_BIAS = 1025;
 
-// DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) is written
-// as u16 (v + 1024; 0xFFFF past the chunk end) to dv[q][chunk * chunk_rows + local row].  Chunk c
+// DENSE = the sample pass: no thresholds; every (query, row) pair's v = dist - pc(q) folds into
+// the lane's running minima (dense_out below), written once per chunk.  Chunk c
 // starts at row row_begin + c * chunk_stride and its tile t at + t * tile_stride: the sample pass
 // spreads 64-row tiles evenly over the whole corpus (tile_stride >= 64, chunk_rows = its tiles x 64
 // dv columns); the thresholded pass uses chunk_stride = chunk_rows and tile_stride = 64.
@@ -154,6 +154,46 @@ constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7, ENT_V_BIAS = 1025;
 // accumulator re-seeds (j = 4+MB, two M-blocks per group); the asynchronous hit flush
 // (gi = 20+MB and 24+MB).
 enum { MFMA_MAIN = 0, MFMA_SAMPLE = 1, MFMA_RERUN = 2 };
+
+// The dense sample pass keeps, per lane and accumulator register, the minimum of v = dist - pc(q)
+// over the sample rows of its chunk that the lane holds (lane row ri of every n-block): 32 values
+// per (query, chunk), each the distance of a DISTINCT sample row, written once per chunk as u16
+// (v + 1024; 0xFFFF: the lane saw no row) to dv[q][col], col = chunk * 32 + ri (DenseMin).  The order
+// statistics sample_select_kernel takes over these minima are >= those over every sample distance:
+// tau_p (K-th + 1) still has K distinct rows below it, and tau_s only admits more rows (the recheck
+// proves it per query either way).
+constexpr int DMIN_NONE = 0x7000;
+template <bool ON, int MB>
+struct DenseMin {  // the sample pass's lane minima (ON); empty in the thresholded passes
+  int v[MB][16];
+  __device__ __forceinline__ DenseMin() {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) v[m][g] = DMIN_NONE;
+  }
+  // v = pc(r) - 2 <q, r> of the 16 registers of M-block m (a row past the chunk end: no value)
+  __device__ __forceinline__ void fold(const v16f& a, int m, int pc, bool ok) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) v[m][g] = min(v[m][g], ok ? pc - (int)(2.0f * a[g]) : DMIN_NONE);
+  }
+  // -> dv[q][col] as u16 (v + 1024; 0xFFFF: no row), col = chunk * 32 + lane row
+  __device__ __forceinline__ void out(uint16_t* __restrict__ dv, int64_t dv_stride, int64_t col, int qbase, int h,
+                                      int nq) const {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+        if (q < nq) dv[(int64_t)q * dv_stride + col] = v[m][g] >= DMIN_NONE ? (uint16_t)0xFFFF : (uint16_t)(v[m][g] + 1024);
+      }
+  }
+};
+template <int MB>
+struct DenseMin<false, MB> {
+  __device__ __forceinline__ void fold(const v16f&, int, int, bool) {}
+  __device__ __forceinline__ void out(uint16_t*, int64_t, int64_t, int, int, int) const {}
+};
 template <int MODE, int MB>
 __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
@@ -407,15 +447,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     }
   };
   auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
-  // DENSE: all 16 distances of block (m, n-block) -> dv (row lr of the chunk)
+  // DENSE: the 16 values v = dist - pc(q) of block (m, n-block) (row lr of the chunk) fold into this
+  // lane's running minima; only those leave the kernel (dense_out)
+  DenseMin<DENSE, MB> dmin;
   auto block_dense = [&](const v16f& a, int m, int pc, int lr) __attribute__((always_inline)) {
-    const int64_t col = (int64_t)chunk * chunk_rows + lr;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-      const int v = pc - (int)(2.0f * a[g]);
-      if (q < nq) dv[(int64_t)q * dv_stride + col] = lr < nrows ? (uint16_t)(v + 1024) : (uint16_t)0xFFFF;
-    }
+    dmin.fold(a, m, pc, lr < nrows);
   };
 
   // ---- main loop: 32 groups per tile (schedule above) ----
@@ -639,7 +675,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }
   wait_lgkm0();
-  if (!DENSE)
+  if constexpr (DENSE)
+    dmin.out(dv, dv_stride, (int64_t)chunk * 32 + ri, qbase, h, nq);
+  else
     for (int i = l; i < QPW; i += 64) {
       const int q = qbase + i;
       if (q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[i];
@@ -838,14 +876,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
     }
   };
 
-  // DENSE: the 16 distances of M-block m of an n-block -> dv (local row lr of the chunk)
+  // DENSE: the 16 values v = dist - pc(q) of M-block m of an n-block (local row lr of the chunk) fold
+  // into this lane's running minima (as K1m's)
+  DenseMin<DENSE, MB> dmin;
   auto block_dense = [&](const v16f& a, int m, int pc, int lr) __attribute__((always_inline)) {
-    const int64_t col = (int64_t)chunk * chunk_rows + lr;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int q = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-      if (q < nq) dv[(int64_t)q * dv_stride + col] = (uint16_t)(pc - (int)(2.0f * a[g]) + 1024);
-    }
+    dmin.fold(a, m, pc, lr < nrows);
   };
   // ---- main loop over n-blocks; k-step s runs the MB MFMAs of n-block blk on the unpacked dword
   // s of `cur`, while the previous n-block's epilogue, this block's row popcount and the next
@@ -939,7 +974,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
     }
   }
   wait_lgkm0();
-  if (!DENSE)
+  if constexpr (DENSE)
+    dmin.out(dv, dv_stride, (int64_t)chunk * 32 + ri, 0, h, nq);
+  else
     for (int i = l; i < QPW; i += 64)
       if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
 }
@@ -1314,7 +1351,8 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->sample_chunks = (int)nsc;
   p->sample_stride = T * ts;
   p->sample_tile_stride = ts;
-  p->sample = tiles * RT;  // dv columns = sample rows
+  p->sample = tiles * RT;
+  p->dvcols = nsc * 32;  // the dense pass writes 32 lane minima per (query, sample chunk)
   S = p->sample;
   // thresholded pass over all n rows (K1r: one chunk per wave, 1024 waves)
   int64_t want = p->rows ? 256 * MWAVES : 256 / p->nqb;
@@ -1330,10 +1368,10 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   while (capc < 4 * expect && capc < 4096) capc <<= 1;
   p->capc = capc;
   p->j = sample_order((double)K * (double)S / (double)n, K);
-  // workspace: dv [nq][sample] u16 | suffix list [nq][K] | cand [nq][nchunks][capc] |
+  // workspace: dv [nq][dvcols] u16 | suffix list [nq][K] | cand [nq][nchunks][capc] |
   //            list lengths [nq][nchunks] | tau_s, tau_p, rerun [nq] | qbflag [nqb]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  p->off_suffix = al((size_t)nq * p->sample * sizeof(uint16_t));
+  p->off_suffix = al((size_t)nq * p->dvcols * sizeof(uint16_t));
   p->off_cand = p->off_suffix + al((size_t)nq * K * sizeof(uint64_t));
   p->off_cnt = p->off_cand + al((size_t)nq * p->nchunks * p->capc * sizeof(uint64_t));
   p->off_tau = p->off_cnt + al((size_t)nq * p->nchunks * sizeof(int32_t));
@@ -1390,18 +1428,18 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   if ((st & VRQ_SCAN_STAGE_PREFIX) && p.rows_sample) {  // dense sample pass (K1r) + per-query thresholds
     rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>,
               hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
-              p.sample_stride, p.sample_tile_stride, dv, p.sample);
+              p.sample_stride, p.sample_tile_stride, dv, p.dvcols);
     VRQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
+    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.dvcols, q, K, p.j,
                        tau_s, tau_p, rerun, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   } else if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
     hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
                        0, s, codes, n, (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0,
                        p.sample_chunk_rows, p.sample_stride, p.sample_tile_stride, p.sample_chunks, p.nqb_s, none,
-                       none, dv, p.sample);
+                       none, dv, p.dvcols);
     VRQ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.sample, q, K, p.j,
+    hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.dvcols, q, K, p.j,
                        tau_s, tau_p, rerun, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   }

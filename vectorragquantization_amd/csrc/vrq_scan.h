@@ -32,14 +32,15 @@ int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, cons
 
 // ---- K1m: matrix-core scan for large query batches (hamming_mfma.hip) ----
 constexpr int kMfmaMaxK = 128;           // K bound of the path
-constexpr int64_t kMfmaMinSample = 32768;
-constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~1.3 ms at nq = 1024)
+constexpr int64_t kMfmaMinSample = 131072;  // (the sample pass writes lane minima only: a larger sample is cheap)
+constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~0.3 ms of MFMA at nq = 1024)
 constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
 constexpr int kMfmaMinQueries = 1;       // auto-selection threshold on the batch size (K1r below 129)
-constexpr int64_t kMfmaSampleDiv = 32;   // dense threshold sample = n / kMfmaSampleDiv rows
+constexpr int64_t kMfmaSampleDiv = 16;   // dense threshold sample = n / kMfmaSampleDiv rows
 
 struct MfmaPlan {
-  int64_t sample;            // dense sample columns (sample_chunks * sample_chunk_rows)
+  int64_t sample;            // dense sample rows (sample_chunks * sample_chunk_rows)
+  int64_t dvcols;            // dv columns per query: 32 lane minima per sample chunk
   int64_t sample_chunk_rows;
   int64_t sample_stride;     // sample chunk c starts at row c * sample_stride
   int64_t sample_tile_stride;  // rows between consecutive sample tiles (>= 64)
