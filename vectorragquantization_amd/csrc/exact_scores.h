@@ -12,10 +12,16 @@ namespace vrq {
 constexpr int DIM = 1024;        // embedding dim of the fused kernels
 constexpr int DPL = DIM / WAVE;  // dims per lane (16)
 
+// Each score is split into the lane's load of the row (phase*_load: the caller may keep several
+// rows' loads in flight) and the arithmetic on the loaded slice (phase*_from); phase2_dot /
+// phase3_cos / flat_ip are the two in sequence.
+
+// Phase II: this lane's code bytes 2l, 2l+1 (dims 16l..16l+15)
+__device__ __forceinline__ uint16_t phase2_load(const uint8_t* __restrict__ code_row) {
+  return *reinterpret_cast<const uint16_t*>(code_row + 2 * lane_id());
+}
 // Phase II score of one code row for the lane-resident query slice (dims 16l..16l+15).
-__device__ __forceinline__ double phase2_dot(const float (&qv)[DPL], const uint8_t* __restrict__ code_row) {
-  const int l = lane_id();
-  const uint16_t b = *reinterpret_cast<const uint16_t*>(code_row + 2 * l);  // bytes 2l, 2l+1
+__device__ __forceinline__ double phase2_from(const float (&qv)[DPL], uint16_t b) {
   double s = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
@@ -25,11 +31,16 @@ __device__ __forceinline__ double phase2_dot(const float (&qv)[DPL], const uint8
   }
   return wave_sum_f64(s);
 }
+__device__ __forceinline__ double phase2_dot(const float (&qv)[DPL], const uint8_t* __restrict__ code_row) {
+  return phase2_from(qv, phase2_load(code_row));
+}
 
+// Phase III: this lane's 16 int8 values of the row
+__device__ __forceinline__ int4 phase3_load(const int8_t* __restrict__ xrow) {
+  return *reinterpret_cast<const int4*>(xrow + DPL * lane_id());
+}
 // Phase III: float32(q . int8 row) / norm, -inf if norm == 0.
-__device__ __forceinline__ double phase3_cos(const float (&qv)[DPL], const int8_t* __restrict__ xrow, double nrm) {
-  const int l = lane_id();
-  const int4 raw = *reinterpret_cast<const int4*>(xrow + DPL * l);
+__device__ __forceinline__ double phase3_from(const float (&qv)[DPL], const int4 raw, double nrm) {
   const int32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
   double s = 0.0;
 #pragma unroll
@@ -41,22 +52,37 @@ __device__ __forceinline__ double phase3_cos(const float (&qv)[DPL], const int8_
   const float f = (float)s;           // one rounding: correctly rounded float32 dot
   return nrm == 0.0 ? -__builtin_inf() : (double)f / nrm;
 }
+__device__ __forceinline__ double phase3_cos(const float (&qv)[DPL], const int8_t* __restrict__ xrow, double nrm) {
+  return phase3_from(qv, phase3_load(xrow), nrm);
+}
 
 // IndexFlatIP (CohereVectorDBFloat.py:62,156): the float32 inner product q . x, computed as the
 // exact products summed in float64 and rounded once to float32 (FAISS's sgemm / fvec_inner_product
 // round at every step; this is the same value within the float32 summation error).
-__device__ __forceinline__ double flat_ip(const float (&qv)[DPL], const float* __restrict__ xrow) {
+struct FlatSlice {
+  float4 v[DPL / 4];
+};
+__device__ __forceinline__ FlatSlice flat_load(const float* __restrict__ xrow) {
   const float4* p = reinterpret_cast<const float4*>(xrow + DPL * lane_id());
+  FlatSlice x;
+#pragma unroll
+  for (int i = 0; i < DPL / 4; ++i) x.v[i] = p[i];
+  return x;
+}
+__device__ __forceinline__ double flat_from(const float (&qv)[DPL], const FlatSlice& x) {
   double s = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL / 4; ++i) {
-    const float4 v = p[i];
+    const float4 v = x.v[i];
     s += (double)qv[4 * i + 0] * (double)v.x;
     s += (double)qv[4 * i + 1] * (double)v.y;
     s += (double)qv[4 * i + 2] * (double)v.z;
     s += (double)qv[4 * i + 3] * (double)v.w;
   }
   return (double)(float)wave_sum_f64(s);
+}
+__device__ __forceinline__ double flat_ip(const float (&qv)[DPL], const float* __restrict__ xrow) {
+  return flat_from(qv, flat_load(xrow));
 }
 
 __device__ __forceinline__ void load_q(float (&qv)[DPL], const float* __restrict__ q) {

@@ -682,15 +682,49 @@ struct Rows {
   const float* xf;       // VRQ_GEMM_FLOAT_IP: float32 rows
 };
 
+// The exact score of one row in two halves: the lane's load of the row (so a wave can keep several
+// candidates' loads in flight) and the arithmetic (exact_scores.h, bit-identical to the fused search).
 template <int PH>
-__device__ __forceinline__ double exact_score(const float (&qv)[DPL], const Rows& c, int64_t row) {
-  if constexpr (PH == VRQ_GEMM_BINARY)
-    return phase2_dot(qv, c.codes + row * (DIM / 8));
-  else if constexpr (PH == VRQ_GEMM_FLOAT_IP)
-    return flat_ip(qv, c.xf + row * DIM);
-  else
-    return phase3_cos(qv, c.x8 + row * DIM, c.norms[row]);
+struct RowSlice {
+  int4 x;      // Phase III: the lane's 16 int8 values
+  double nrm;  //   ... and the row's norm
+};
+template <>
+struct RowSlice<VRQ_GEMM_BINARY> {
+  uint16_t b;  // the lane's two code bytes
+};
+template <>
+struct RowSlice<VRQ_GEMM_FLOAT_IP> {
+  FlatSlice x;  // the lane's 16 floats
+};
+template <int PH>
+__device__ __forceinline__ RowSlice<PH> load_row(const Rows& c, int64_t row) {
+  RowSlice<PH> d;
+  if constexpr (PH == VRQ_GEMM_BINARY) {
+    d.b = phase2_load(c.codes + row * (DIM / 8));
+  } else if constexpr (PH == VRQ_GEMM_FLOAT_IP) {
+    d.x = flat_load(c.xf + row * DIM);
+  } else {
+    d.x = phase3_load(c.x8 + row * DIM);
+    d.nrm = c.norms[row];
+  }
+  return d;
 }
+template <int PH>
+__device__ __forceinline__ double score_row(const float (&qv)[DPL], const RowSlice<PH>& d) {
+  if constexpr (PH == VRQ_GEMM_BINARY)
+    return phase2_from(qv, d.b);
+  else if constexpr (PH == VRQ_GEMM_FLOAT_IP)
+    return flat_from(qv, d.x);
+  else
+    return phase3_from(qv, d.x, d.nrm);
+}
+// candidate rows a wave scores per round, all loads issued before the first score.  Measured at
+// 10M rows (c5): 8 rows per round made the finish SLOWER (cosine 1.21 -> 1.79 ms, binary 1.07 ->
+// 1.25 ms): 210 VGPRs cut the resident workgroups per CU, and the co-resident waves already hide the
+// gathers' latency at one row per round.
+template <int PH>
+constexpr int kScoreBatch = 1;
 
 // Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
@@ -707,14 +741,25 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
     const uint64_t kk = kc == k ? key[k - 1] : KEY_NONE;
     const uint32_t kr = kc == k ? row[k - 1] : 0xffffffffu;
     const int64_t end = base + FB_BATCH < count ? base + FB_BATCH : count;
-    for (int64_t j = base + w; j < end; j += 4) {
-      const uint32_t rr = row_at(j);
-      const uint64_t key_r = desc_key_f64(exact_score<PH>(qv, c, (int64_t)rr));
-      const bool take = kc < k || key_r < kk || (key_r == kk && rr < kr);
-      if (take && l == 0) {
-        const int i = kc + atomicAdd(fill, 1);
-        key[i] = key_r;
-        row[i] = rr;
+    constexpr int U = kScoreBatch<PH>;
+    for (int64_t j0 = base + w; j0 < end; j0 += 4 * U) {  // this wave: j0, j0 + 4, ... (wave-uniform)
+      uint32_t rr[U];
+      RowSlice<PH> d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) rr[u] = j0 + 4 * u < end ? row_at(j0 + 4 * u) : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j0 + 4 * u < end) d[u] = load_row<PH>(c, (int64_t)rr[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j0 + 4 * u >= end) break;
+        const uint64_t key_r = desc_key_f64(score_row<PH>(qv, d[u]));
+        const bool take = kc < k || key_r < kk || (key_r == kk && rr[u] < kr);
+        if (take && l == 0) {
+          const int i = kc + atomicAdd(fill, 1);
+          key[i] = key_r;
+          row[i] = rr[u];
+        }
       }
     }
     __syncthreads();

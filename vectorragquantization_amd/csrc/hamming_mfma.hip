@@ -458,7 +458,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   v4i ring[NRING];
   const uint32_t bl0 = ub0 + (uint32_t)(l * 16);  // + tile slot + group * 1024: this lane's B fragment
   int pcvP = 0;  // previous tile's n-block 1 row popcount
-  uint64_t hitm = 0;  // lanes of the previous n-block with a candidate in some M-block (wave-uniform)
+  uint64_t hitm[MB];  // per M-block: lanes of the previous n-block with a candidate (wave-uniform)
+#pragma unroll
+  for (int m = 0; m < MB; ++m) hitm[m] = 0;
   int hpb = 0;   // the previous n-block's per-lane threshold pc(r)/2, as float bits
   v16f acc[2][MB];  // [n-block][m]
   if constexpr (!DENSE)
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             f0 = max(max(e0, e1), e2);
             asm volatile("" : "+v"(e4), "+v"(f0));
           } else {
-            hitm |= __ballot(max(max(e3, e4), max(bb[15], f0)) > hpb);
+            hitm[tm] = __ballot(max(max(e3, e4), max(bb[15], f0)) > hpb);
           }
         }
         if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 1 && k == 0) {
@@ -611,18 +613,20 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 127) * 4), l < nfl ? 1 : 0);
           // hit extraction of the previous n-block's flagged M-blocks, once per n-block (rare)
           if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 3 + MB) {
-            if (hitm) {
+            // (hitm[m] is assigned by every n-block's test of M-block m before this point)
+            uint64_t any = hitm[0];
+#pragma unroll
+            for (int m = 1; m < MB; ++m) any |= hitm[m];
+            if (any) {
               const int pcr_ = nbk == 0 ? pcvP : pcv[0];
               const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
               const int pc = row_pc(pcr_, lr);
               const float hp = 0.5f * (float)pc;
               static_for<0, MB>([&](auto M) {
                 constexpr int mm = decltype(M)::value;
-                if (any_above(acc[nbk ^ 1][mm], hp))
-                  block_hits(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
+                if (hitm[mm]) block_hits(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
               });
             }
-            hitm = 0;
           }
         }
       };
@@ -888,7 +892,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
   int pcs = 0;       // running row popcount of this n-block (this lane's half)
   int pprev = 0;     // the previous n-block's row popcount (whole row)
   int hpb = 0x7fffffff;
-  uint64_t hitm = 0;
+  uint64_t hitm[MB];  // per M-block: lanes of the previous n-block with a candidate (wave-uniform)
+#pragma unroll
+  for (int m = 0; m < MB; ++m) hitm[m] = 0;
   auto nblock = [&](auto PAR, int blk) __attribute__((always_inline)) {
     constexpr int par = decltype(PAR)::value;  // blk & 1 (n-blocks run in pairs: static accumulator indices)
     // the next n-block's tile: its DMA landed (tile boundary), and the ring slot of tile t+NPR-1 ...
@@ -923,20 +929,22 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
         const int x0 = max(max(bb[0], bb[1]), bb[2]), x1 = max(max(bb[3], bb[4]), bb[5]);
         const int x2 = max(max(bb[6], bb[7]), bb[8]), x3 = max(max(bb[9], bb[10]), bb[11]);
         const int x4 = max(max(bb[12], bb[13]), bb[14]);
-        hitm |= __ballot(max(max(max(x0, x1), x2), max(max(x3, x4), bb[15])) > hpb);
+        hitm[m] = __ballot(max(max(max(x0, x1), x2), max(max(x3, x4), bb[15])) > hpb);
       }
       if constexpr (!DENSE && s == MB + 1) {
-        if (hitm) {  // rare
+        uint64_t any = hitm[0];  // (every hitm[m] assigned by this n-block's tests)
+#pragma unroll
+        for (int m = 1; m < MB; ++m) any |= hitm[m];
+        if (any) {  // rare
           const int lrp = lr - 32;
           const int pc = lrp < nrows && blk > 0 ? pprev : 0x40000000;
           const float hp = 0.5f * (float)pc;
           static_for<0, MB>([&](auto M) {
             constexpr int mm = decltype(M)::value;
-            if (any_above(acc[par ^ 1][mm], hp)) block_hits(acc[par ^ 1][mm], mm, pc, hp);
+            if (hitm[mm]) block_hits(acc[par ^ 1][mm], mm, pc, hp);
           });
           if (nst) flush_all(row0 + (int64_t)(blk - 1) * 32);
         }
-        hitm = 0;
       }
       if constexpr (!DENSE && s >= MB + 2 && s < 2 * MB + 2) load_seed(acc[par ^ 1][s - MB - 2], s - MB - 2);
       // the next n-block's packed data
