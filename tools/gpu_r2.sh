@@ -10,6 +10,8 @@ mkdir -p $OUT
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${TEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -60 $OUT/pytest_gpu.log; exit 1; }
   tail -3 $OUT/pytest_gpu.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $OUT/smoke.log; exit 1; }
+  tail -1 $OUT/smoke.log
 fi
 for c in ${BENCHES:-c4}; do
   timeout -k 10 ${BENCH_T:-600} python -u bench.py --config $c ${BENCH_EXTRA:-} > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { echo BENCH_FAIL $c; tail -30 $OUT/bench_$c.err; exit 1; }
