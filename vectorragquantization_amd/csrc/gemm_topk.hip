@@ -13,7 +13,7 @@
 //     a power of two) and rho the exact residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
 //     s' the reference score in the same units (Phase III: s/S; Phase II: (s + sum q)/(2S)):
 //       Phase III  Delta = ||rho||_2 (Cauchy-Schwarz; the score divides by ||x||_2) + f32 slack
-//       Phase II   Delta = ||rho||_1 (x in {0,1})                                  + f32 slack
+//       Phase II   Delta = max(sum rho+, sum rho-) (x in {0,1}: <rho, x> lies between them) + f32 slack
 //  2. sample pass (dense): u for every (query, row) of an evenly spread row sample, where
 //     u = fl(A_0 [+ A_1/256]) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
 //     (x = the int8 row, or the code's bits expanded to 0/1 bytes).  Only the running max of u per
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     while ((double)mx <= 127.0 * ldexp(1.0, e - 1)) --e;
   }
   const double invS = NPC == 2 ? ldexp(1.0, -e) : (mx > 0.f ? 127.0 / (double)mx : 1.0);
-  double r2 = 0.0, r1 = 0.0, q2 = 0.0, q1 = 0.0, qs = 0.0;
+  double r2 = 0.0, rp = 0.0, rn = 0.0, q2 = 0.0, q1 = 0.0, qs = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const double x = (double)qv[i] * invS;  // exact for two pieces
@@ -181,7 +181,8 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     b = b > 127.0 ? 127.0 : (b < -127.0 ? -127.0 : b);
     const double rho = f - b * (1.0 / 256.0);  // exact
     r2 += rho * rho;
-    r1 += fabs(rho);
+    rp += rho > 0.0 ? rho : 0.0;
+    rn += rho < 0.0 ? -rho : 0.0;
     q2 += (double)qv[i] * (double)qv[i];
     q1 += fabs((double)qv[i]);
     qs += (double)qv[i];
@@ -191,7 +192,8 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     if (NPC == 2) o[1024 + pos] = (int8_t)b;
   }
   r2 = wave_sum_f64(r2);
-  r1 = wave_sum_f64(r1);
+  rp = wave_sum_f64(rp);
+  rn = wave_sum_f64(rn);
   q2 = wave_sum_f64(q2);
   q1 = wave_sum_f64(q1);
   qs = wave_sum_f64(qs);
@@ -199,7 +201,9 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   if (l == 0) {
     double d;
     if (mode == VRQ_GEMM_BINARY) {
-      d = r1 * (1.0 + SLACK) + SLACK * q1 * invS;
+      // x in {0, 1}: u - s' = -<rho, x> lies in [-sum rho+, sum rho-], so |u - s'| <= max of the
+      // two one-sided sums (about half of ||rho||_1)
+      d = fmax(rp, rn) * (1.0 + SLACK) + SLACK * q1 * invS;
     } else if (mode == VRQ_GEMM_FLOAT_IP) {
       // u = s_r <a, b_r> against s' = <q/S, x_r> with x_r = s_r b_r + sigma_r (flat_ip_prepare):
       // |u - s'| <= ||rho|| ||s_r b_r|| + ||q/S|| ||sigma_r|| <= ||rho|| Bx + ||q/S|| Bsigma, and
