@@ -724,11 +724,18 @@ __device__ __forceinline__ double score_row(const float (&qv)[DPL], const RowSli
     return phase3_from(qv, d.x, d.nrm);
 }
 // candidate rows a wave scores per round, all loads issued before the first score.  Measured at
-// 10M rows (c5): 8 rows per round made the finish SLOWER (cosine 1.21 -> 1.79 ms, binary 1.07 ->
-// 1.25 ms): 210 VGPRs cut the resident workgroups per CU, and the co-resident waves already hide the
-// gathers' latency at one row per round.
+// 10M rows (c5 finish, ms per 1024 queries; profiles/r2s3/c5_finish_score_batch.jsonl):
+//   binary  1 row 0.89, 2 rows 0.78, 3 rows 0.75, 8 rows 1.25
+//   cosine  1 row 1.23, 2 rows 1.13, 3 rows 1.15, 8 rows 1.79
+// (more rows per round cost VGPRs and with them resident workgroups per CU).  VRQ_G5_SCORE_BATCH
+// overrides it in probe builds (tools/build_g5_variants.sh).
 template <int PH>
-constexpr int kScoreBatch = 1;
+constexpr int kScoreBatch =
+#ifdef VRQ_G5_SCORE_BATCH
+    VRQ_G5_SCORE_BATCH;
+#else
+    PH == VRQ_GEMM_BINARY ? 3 : 2;
+#endif
 
 // Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
