@@ -225,3 +225,24 @@ def test_mfma_sampled_threshold_rerun(dev, oracle_lib, nq):
     assert (D0[0] == 30).sum() == 30 and (D0[nq - 10] == 30).sum() == 30
     assert np.array_equal(D0, D1)
     assert np.array_equal(I0, I1)
+
+
+@pytest.mark.parametrize("nq", [40, 130, 520])
+def test_mfma_cluster_ordered_corpus(dev, oracle_lib, nq):
+    """Corpus stored in cluster order (1000 contiguous near-copies of each centre): a query's whole
+    neighbourhood sits in one chunk and in few lane rows of the sample, so the sample pass's lane
+    minima collapse many near rows into one value each (looser tau_s / tau_p).  The result must
+    still be exactly the FAISS order (recheck + re-run + suffix); covers K1r (40 queries), the
+    MB = 2 (130) and MB = 4 (520) instances of K1m."""
+    rng = np.random.default_rng(4242 + nq)
+    ncl, per = 300, 1000
+    centres = rng.integers(0, 256, (ncl, 128), dtype=np.uint8)
+    bits = np.unpackbits(np.repeat(centres, per, axis=0), axis=1)
+    flips = rng.random(bits.shape) < rng.uniform(0.01, 0.06, (bits.shape[0], 1))
+    codes = np.packbits(bits ^ flips, axis=1)
+    qb = _near(rng, centres[rng.integers(0, ncl, nq)], 12)
+    D0, I0 = oracle_knn(oracle_lib, codes, qb, 100)
+    c, D1, I1 = _phase1(codes, qb, 100, dev, "mfma")
+    assert np.array_equal(c, np.full(nq, 100))
+    assert np.array_equal(D0, D1)
+    assert np.array_equal(I0, I1)
