@@ -13,7 +13,8 @@ if [ -n "${G5_ENVS+x}" ]; then
   cat $OUT/g5.jsonl
 fi
 for e in ${C2_ENVS:-}; do
-  env $(echo $e | tr ',' ' ') timeout -k 10 200 python -u bench.py --config ${C2_CFG:-c2} --no-cpu-baseline --no-recall --no-encode --steps 20 --warmup 3 > $OUT/c2_$e.json 2> $OUT/c2_$e.err || { echo C2_FAIL $e; tail -20 $OUT/c2_$e.err; exit 1; }
-  python -c "import json;d=json.load(open('$OUT/c2_$e.json'));print('$e', round(d['ms_per_step'],4), {k:round(v,4) for k,v in d['phase_ms'].items()}, round(d['roofline']['frac'],3))"
+  f=$OUT/c2_${e//\//_}
+  env $(echo $e | tr ',' ' ') timeout -k 10 200 python -u bench.py --config ${C2_CFG:-c2} --no-cpu-baseline --no-recall --no-encode --steps 20 --warmup 3 > $f.json 2> $f.err || { echo C2_FAIL $e; tail -20 $f.err; exit 1; }
+  python -c "import json;d=json.load(open('$f.json'));print('$e', round(d['ms_per_step'],4), {k:round(v,4) for k,v in d['phase_ms'].items()}, round(d['roofline']['frac'],3))"
 done
 echo done

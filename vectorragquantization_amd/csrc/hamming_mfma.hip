@@ -701,6 +701,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 // Same thresholds (sampled tau_s / exact re-run with tau_p), same per-(query, chunk) lists and
 // suffix merge as K1m; the hit path flushes synchronously (hits are rare at the sizes this serves).
 constexpr int NPR = 3;  // per-wave packed ring depth (tile t+2 in flight while tile t is read)
+// cache-policy bits of K1r's LDS-DMA: 2 = nt (each row is read by one wave once per batch).  c3
+// (100M rows, nq = 8): 2.11 -> 2.02 ms per pass, 0.76 -> 0.79 of HBM (profiles/r2s3/c3_k1r_nt.txt)
+#ifndef VRQ_K1R_AUX
+#define VRQ_K1R_AUX 2
+#endif
 template <int MB>
 struct RowsShape {
   static constexpr int QPW = 32 * MB;
@@ -758,7 +763,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + i * 1024), 16,
-                                         0, 0);
+                                         0, VRQ_K1R_AUX);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
