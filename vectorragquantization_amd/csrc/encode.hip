@@ -29,7 +29,31 @@ struct PwPlan {
   int16_t start[MAX_LEAVES];
   int16_t len[MAX_LEAVES];
   int16_t ops[MAX_OPS];  // postfix: >= 0 push leaf sum, -1 add the top two
+  int bal_levels;        // L when the tree is the balanced one over 2^L <= 8 leaves in order, else -1
 };
+
+// postfix of the balanced tree over leaves [first, first + 2^L): left, right, add
+static void pw_balanced(int first, int L, int16_t* ops, int* k) {
+  if (L == 0) {
+    ops[(*k)++] = (int16_t)first;
+    return;
+  }
+  pw_balanced(first, L - 1, ops, k);
+  pw_balanced(first + (1 << (L - 1)), L - 1, ops, k);
+  ops[(*k)++] = -1;
+}
+static void pw_classify(PwPlan* p) {
+  p->bal_levels = -1;
+  for (int L = 0; L <= 3; ++L) {
+    if (p->nleaves != (1 << L)) continue;
+    int16_t ops[16];
+    int k = 0;
+    pw_balanced(0, L, ops, &k);
+    bool same = k == p->nops;
+    for (int i = 0; same && i < k; ++i) same = ops[i] == p->ops[i];
+    if (same) p->bal_levels = L;
+  }
+}
 
 static void pw_build(int s, int n, PwPlan* p) {
   if (n <= 128) {
@@ -45,9 +69,21 @@ static void pw_build(int s, int n, PwPlan* p) {
   p->ops[p->nops++] = -1;
 }
 
+// The encoder runs one WAVE per vector, EPB vectors per workgroup (fewer, larger workgroups: with
+// one 64-thread workgroup per vector the dispatch of ~1M workgroups bounded the launch), each wave
+// on its own LDS slice; LDS is shared only inside a wave, so the wave orders its own accesses.
+constexpr int EPB = 1;  // 4 measured ~15 % slower (int8g 1.42 -> 1.65 ms per 2^20 vectors)
+// (Padding the LDS image by 8 floats per 128 elements, against the bank pattern of the leaf reads,
+// measured 4-11 % slower and is not used.)
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // NumPy pairwise float32 sum of x[0..n) staged in LDS; result valid in all lanes.
 __device__ float pairwise_sum_f32(const float* x, const PwPlan& P, float* leafsum) {
   const int l = lane_id(), g = l >> 3, j = l & 7;
+  float lastres = 0.f;  // lanes 8g: the sum of leaf b + g of the last batch
   for (int b = 0; b < P.nleaves; b += 8) {
     const int li = b + g;
     float r = 0.f;
@@ -76,9 +112,20 @@ __device__ float pairwise_sum_f32(const float* x, const PwPlan& P, float* leafsu
       }
       for (; i < m; ++i) res += x[s + i];
       leafsum[li] = res;
+      lastres = res;
     }
   }
-  __syncthreads();
+  if (P.bal_levels >= 0) {
+    // the balanced tree over <= 8 leaves (dim = 1024: ((L0+L1)+(L2+L3))+((L4+L5)+(L6+L7))), one
+    // batch, leaf g in lane 8g: a butterfly over xor 8, 16, 32 performs exactly the tree's additions
+    // (float addition is commutative; the association is the tree's)
+    float a = lastres;
+    if (P.bal_levels >= 1) a = a + __shfl_xor(a, 8, WAVE);
+    if (P.bal_levels >= 2) a = a + __shfl_xor(a, 16, WAVE);
+    if (P.bal_levels >= 3) a = a + __shfl_xor(a, 32, WAVE);
+    return __shfl(a, 0, WAVE);
+  }
+  wave_lds_sync();
   float out = 0.f;
   if (l == 0) {
     float* st = leafsum + MAX_LEAVES;  // LDS stack (no scratch)
@@ -101,12 +148,15 @@ __device__ float pairwise_sum_f32(const float* x, const PwPlan& P, float* leafsu
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
 template <int MODE>
-__global__ __launch_bounds__(64) void encode_kernel(const void* __restrict__ xin, int64_t n, int dim, double limit,
-                                                    uint8_t* __restrict__ codes, void* __restrict__ qout,
-                                                    double* __restrict__ minmax, PwPlan P) {
-  extern __shared__ __attribute__((aligned(16))) float xs[];  // dim floats + leaf sums
+__global__ __launch_bounds__(EPB * 64) void encode_kernel(const void* __restrict__ xin, int64_t n, int dim,
+                                                          double limit, uint8_t* __restrict__ codes,
+                                                          void* __restrict__ qout, double* __restrict__ minmax,
+                                                          PwPlan P, int epb) {
+  extern __shared__ __attribute__((aligned(16))) float smem_enc[];
+  const int w = threadIdx.x >> 6;
+  float* xs = smem_enc + w * (dim + 2 * MAX_LEAVES);  // this wave's dim floats + leaf sums
   float* leafsum = xs + dim;
-  const int64_t v = blockIdx.x;
+  const int64_t v = (int64_t)blockIdx.x * epb + w;
   if (v >= n) return;
   const int l = lane_id();
   const int ngroups = dim / 8;
@@ -115,6 +165,25 @@ __global__ __launch_bounds__(64) void encode_kernel(const void* __restrict__ xin
   if constexpr (MODE == VRQ_ENC_BIN_INT16) {
     // VectorDBInt16._to_binary: float64 mean of int16 (exact sum), x > mean
     const int16_t* x = reinterpret_cast<const int16_t*>(xin) + v * dim;
+    if (dim == 16 * WAVE) {  // d = 1024: lane l holds elements 16l..16l+15 (two 16-B loads)
+      const int4* p = reinterpret_cast<const int4*>(x + 16 * l);
+      const int4 a = p[0], b = p[1];
+      const uint32_t wv[8] = {(uint32_t)a.x, (uint32_t)a.y, (uint32_t)a.z, (uint32_t)a.w,
+                              (uint32_t)b.x, (uint32_t)b.y, (uint32_t)b.z, (uint32_t)b.w};
+      int e[16];
+      int32_t ls = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        e[k] = (int)(int16_t)(wv[k >> 1] >> (16 * (k & 1)));
+        ls += e[k];
+      }
+      const double mean = (double)wave_sum_i64((int64_t)ls) / (double)dim;  // exact sum, one rounding
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) bits |= ((double)e[k] > mean ? 1u : 0u) << ((k < 8 ? 7 - k : 23 - k));
+      *reinterpret_cast<uint16_t*>(crow + 2 * l) = (uint16_t)bits;  // bytes 2l (elements 0..7), 2l+1
+      return;
+    }
     int64_t s = 0;
     for (int i = l; i < dim; i += WAVE) s += x[i];
     s = wave_sum_i64(s);
@@ -129,7 +198,7 @@ __global__ __launch_bounds__(64) void encode_kernel(const void* __restrict__ xin
   } else {
     const float* x = reinterpret_cast<const float*>(xin) + v * dim;
     for (int i = 4 * l; i < dim; i += 4 * WAVE) *reinterpret_cast<float4*>(xs + i) = *reinterpret_cast<const float4*>(x + i);
-    __syncthreads();
+    wave_lds_sync();
     float mean = 0.f;
     if constexpr (MODE != VRQ_ENC_COHERE) {
       const float s = pairwise_sum_f32(xs, P, leafsum);
@@ -281,10 +350,14 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
   if (mode == VRQ_ENC_INT8_LOCAL || mode == VRQ_ENC_INT4_LOCAL) VRQ_CHECK_ARG(minmax);
   PwPlan P{};
   pw_build(0, dim, &P);
+  pw_classify(&P);
   if (P.nleaves > MAX_LEAVES) return VRQ_EUNSUPPORTED;
-  const size_t lds = sizeof(float) * (dim + 2 * MAX_LEAVES);
+  // EPB vectors per workgroup while their LDS slices stay within 64 KiB (dim <= 3840), else one
+  const int epb = sizeof(float) * EPB * (dim + 2 * MAX_LEAVES) <= 65536 ? EPB : 1;
+  const size_t lds = sizeof(float) * epb * (dim + 2 * MAX_LEAVES);
   hipStream_t s = (hipStream_t)stream;
-  // one wave per vector; launches of at most 2^24 vectors keep a dispatch below 2^32 work-items
+  // one wave per vector (EPB per workgroup); launches of at most 2^24 vectors keep a dispatch below
+  // 2^32 work-items
   const int64_t xrow = (int64_t)dim * (mode == VRQ_ENC_BIN_INT16 ? 2 : 4);
   const int64_t qrow = mode == VRQ_ENC_INT16_GLOBAL                              ? 2 * (int64_t)dim
                        : (mode == VRQ_ENC_INT4_GLOBAL || mode == VRQ_ENC_INT4_LOCAL) ? (int64_t)(dim + 1) / 2
@@ -296,28 +369,28 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
     uint8_t* cv = codes + v0 * (dim / 8);
     void* qv = q ? (void*)((uint8_t*)q + v0 * qrow) : nullptr;
     double* mv = minmax ? minmax + 2 * v0 : nullptr;
-    const dim3 grid((unsigned)nv), block(64);
+    const dim3 grid((unsigned)((nv + epb - 1) / epb)), block(epb * 64);
     switch (mode) {
       case VRQ_ENC_INT8_GLOBAL:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       case VRQ_ENC_INT16_GLOBAL:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       case VRQ_ENC_INT4_GLOBAL:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       case VRQ_ENC_INT8_LOCAL:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       case VRQ_ENC_INT4_LOCAL:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       case VRQ_ENC_BIN_INT16:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_BIN_INT16>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_BIN_INT16>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
       default:
-        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_COHERE>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P);
+        hipLaunchKernelGGL(encode_kernel<VRQ_ENC_COHERE>, grid, block, lds, s, xv, nv, dim, limit, cv, qv, mv, P, epb);
         break;
     }
     VRQ_LAUNCH_CHECK();
