@@ -944,7 +944,9 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   if (S < kMinSample) S = kMinSample;
   if (S > kMaxSample) S = kMaxSample;
   if (S > n) S = n;
-  int64_t nsc = want;
+  // sample chunks: one per CU and query block, and >= 2k / 32 so the select sees >= 2k lane maxima
+  // per query (fewer than k would leave thr = -inf: every row a candidate)
+  int64_t nsc = want > (2 * (int64_t)k + GRT - 1) / GRT ? want : (2 * (int64_t)k + GRT - 1) / GRT;
   int64_t scr = ((S + nsc - 1) / nsc + GRT - 1) / GRT * GRT;
   nsc = (S + scr - 1) / scr;
   p->scr = scr;

@@ -1355,7 +1355,9 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   // spill in the dense epilogue, so batches of 65..128 queries take K1m's (MB = 2) sample pass
   p->rows_sample = p->rows && p->mb <= 2;
   int64_t nsc = p->rows_sample ? 256 * MWAVES : 256 / p->nqb_s;
-  if (nsc < 1) nsc = 1;
+  // >= 8 chunks: >= 256 lane minima per query (>= 2K; very large batches would otherwise keep
+  // fewer than K values and fall back to accepting every row)
+  if (nsc < 8) nsc = 8;
   if (nsc > tiles) nsc = tiles;
   const int64_t T = tiles / nsc;
   tiles = nsc * T;
