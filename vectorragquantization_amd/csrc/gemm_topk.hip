@@ -221,9 +221,9 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
 }
 
 // ---------------------------------------------------------------------------------------------
-// The matrix pass.  PH = VRQ_GEMM_BINARY / VRQ_GEMM_INT8_COSINE; DENSE = the sample pass (u of
-// every (query, row) -> dv[q][chunk * chunk_rows + row]) else the thresholded pass (u >= thr[q] ->
-// candidate lists).  Chunk c covers rows [c * chunk_stride, + chunk_rows).
+// The matrix pass.  PH = VRQ_GEMM_BINARY / VRQ_GEMM_INT8_COSINE; DENSE = the sample pass (the max
+// of u over each lane row's rows of the chunk -> dv[q][chunk * 32 + lane row]) else the thresholded
+// pass (u >= thr[q] -> candidate lists).  Chunk c covers rows [c * chunk_stride, + chunk_rows).
 // RETRY: the retry pass of launch_finish (same code; a separate symbol so kernel traces and counter
 // summaries keep the main pass's per-launch figures apart from the retry's near-empty launch).
 template <int PH, bool DENSE, bool RETRY = false>

@@ -720,7 +720,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   // DENSE = the sample pass (as K1m's): chunk c = this wave's T tiles, tile t at row
-  // c * chunk_stride + t * tile_stride (every tile whole), u16 distances to dv[q][c * chunk_rows + row]
+  // c * chunk_stride + t * tile_stride (every tile whole), lane minima to dv[q][c * 32 + lane row]
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
   constexpr int QPW = RowsShape<MB>::QPW;
   if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
