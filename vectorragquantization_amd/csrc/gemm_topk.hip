@@ -60,6 +60,9 @@
 #ifndef VRQ_G5_PIECES
 #define VRQ_G5_PIECES 1
 #endif
+#ifndef VRQ_G5_NORM_REG
+#define VRQ_G5_NORM_REG 0  // Phase III: the tile's norms by a plain global load into registers (1) instead of LDS-DMA
+#endif
 
 namespace vrq {
 namespace g5 {
@@ -239,7 +242,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   constexpr int NP = P3 ? VRQ_G5_NP3 : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
-  constexpr int PPW = P3 ? 9 : 1;                     // LDS-DMA instructions per wave per tile
+  constexpr int PPW = P3 ? 9 : 1;                     // vector-memory instructions per wave per tile
+  constexpr bool NREG = P3 && VRQ_G5_NORM_REG;        // (8 LDS-DMA rows + 1 norm load, or 9 LDS-DMA)
   constexpr int AHEAD = NP - 1;                       // tiles the DMA runs ahead
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   __shared__ int32_t lcnt[GW * GQW];  // per-(query, this chunk) list lengths, one row of 32 per wave
@@ -335,9 +339,21 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     lds_write128(ubw + (uint32_t)(((4 * uc + i) * 64 + hh * 32 + r) * 16), f);
   };
 
+  // NREG: this lane's row norm of a tile (tile row r; both lane halves load the same) into a
+  // register, issued before the tile's 8 row pieces so the per-tile vmcnt accounting is unchanged
+  double nvr[2] = {0.0, 0.0};  // by tile parity: tile t's norm, loaded during tile t - 2
+  auto issue_norm = [&](int tt, double& dst) {
+    const double* base = norms + row0 + tstart(tt);
+    const uint32_t off = (uint32_t)((tiny ? (r < nrows ? r : nrows - 1) : r) * 8);
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(dst) : "v"(off), "s"(base) : "memory");
+  };
   for (int t = 0; t < AHEAD && t < ntiles; ++t) {
+    if constexpr (NREG) {
+      if (t == 0) issue_norm(0, nvr[0]);
+      else issue_norm(1, nvr[1]);
+    }
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
+    for (int i = 0; i < (NREG ? 8 : PPW); ++i) {
       if (tiny)
         issue_tiny(i);
       else
@@ -471,7 +487,12 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     v4i pv = {};
     const uint32_t ubn = sm0 + (uint32_t)(NP * T2 + ((t + 1) & 1) * U2);  // Phase II: tile t+1 expanded here
     uint32_t badr[8];
-    if constexpr (P3) {
+    if constexpr (NREG) {
+      asm volatile("" : "+v"(nvr[p]));  // landed: older than the tile's row pieces the wait covered
+      nv = nvr[p];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
+    } else if constexpr (P3) {
       lds_read64(nv, slot + T3 + (uint32_t)(r * 8));
 #pragma unroll
       for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
@@ -510,9 +531,12 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
       // DMA of tile t + AHEAD, spread over the MFMA shadow
       if constexpr (P3) {
-        constexpr int DS = VRQ_G5_DMA_STRIDE;
-        if constexpr (s >= 2 && s < 2 + DS * 9 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2))
+        constexpr int DS = VRQ_G5_DMA_STRIDE, NPC3 = NREG ? 8 : 9;
+        if constexpr (s >= 2 && s < 2 + DS * NPC3 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2)) {
+          if constexpr (NREG && s == 2)
+            if (dma) issue_norm(t + AHEAD, nvr[p]);  // (nv holds this tile's norm already)
           if (dma) issue_piece(dt, (s - 2) / DS);
+        }
       } else {
         if constexpr (s == 2 && !(VRQ_G5_BISECT & 2))
           if (dma) issue_piece(dt, 0);
