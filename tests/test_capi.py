@@ -53,6 +53,22 @@ def test_workspace_sizes():
     assert 1 <= per_q <= 4096
 
 
+def test_workspace_sizes_lane_extrema_samples():
+    """The sample passes keep 32 lane extrema per (query, sample chunk), not one value per sample
+    row: the workspace no longer scales with nq x S (round 1: nq x S u16 / f32 matrices), and very
+    large batches or k still plan (>= 8 / >= 2k/32 sample chunks)."""
+    lib = N.load()
+    # config 4 shape: the scan workspace is the candidate lists plus a few MB, far below nq x S x 2 B
+    ws4 = lib.vrq_search3_workspace_size(100_000_000, 1024, 1024, 100)
+    assert 0 < ws4 < 1024 * (1 << 20) * 2
+    # config 5 shape: f32 maxima (nq x nsc x 32) instead of nq x S floats (~800 MB at 10M rows)
+    g5 = lib.vrq_gemm_topk_workspace_size(3, 10_000_000, 1024, 1024, 10)
+    assert 0 < g5 < 700 << 20
+    # huge batches / large k still produce a plan
+    assert lib.vrq_search3_workspace_size(1_000_000, 1024, 65536, 100) > 0
+    assert lib.vrq_gemm_topk_workspace_size(3, 1_000_000, 1024, 8192, 1000) > 0
+
+
 @pytest.mark.parametrize("call,expect", [
     (lambda L: L.vrq_encode(99, None, 1, 1024, 0.3, None, None, None, None), N.VRQ_EINVAL),
     (lambda L: L.vrq_encode(0, None, -1, 1024, 0.3, None, None, None, None), N.VRQ_EINVAL),
