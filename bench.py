@@ -90,6 +90,7 @@ def parse():
     ap.add_argument("--no-encode", action="store_true", help="skip the encoder roofline leg")
     ap.add_argument("--scan", choices=["auto", "valu", "mfma"], default="auto",
                     help="Phase-I scan (auto = the library's choice for the shape)")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -392,23 +393,28 @@ def encode_roofline(dev, n=1 << 20, reps=5):
     qbytes = {"int8g": 1024, "int16g": 2048, "int4g": 512, "int8": 1024 + 16, "int4": 512 + 16, "bin16": 0,
               "cohere": 1024}
     out = {}
+    lib, st = N.load(), N.stream_handle(dev)
     for mode in ("int8g", "int16g", "int4g", "int8", "int4", "bin16", "cohere"):
         inp = X16 if mode == "bin16" else X
-        encode(mode, inp, 0.1, dev)
+        o = encode(mode, inp, 0.1, dev)  # warm-up launch; its outputs are the preallocated buffers below
+        args = (N.ENC_MODES[mode], N.ptr(inp), n, 1024, 0.1, N.ptr(o["codes"]), N.ptr(o["q"]), N.ptr(o["minmax"]), st)
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
-            encode(mode, inp, 0.1, dev)
+            lib.vrq_encode(*args)  # launches only: no allocation inside the window
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
+        del o
         b = n * ((2048 if mode == "bin16" else 4096) + 128 + qbytes[mode])
         out[mode] = {"ms": ms, "GB/s": b / (ms * 1e-3) / 1e9, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "bytes_per_launch": b}
     del X, X16
     torch.cuda.empty_cache()
     return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "vectors_per_launch": n,
-            "timing": "HIP events around 5 launches (includes the host-side output allocation)", "modes": out}
+            "timing": f"HIP events around {reps} back-to-back vrq_encode launches into preallocated outputs",
+            "modes": out}
 
 
 def pmc_traffic(tag, kernel):
@@ -509,6 +515,38 @@ def cpu_baseline_c5(codes_h, x8_h, qf_h, k, n, nq_s=4, threads=16):
                       f"2*unpackbits-1; float32 dot / float64 norm), {t:.1f} s, scaled by n/{rs}"}
 
 
+def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517)):
+    """Config-5 identity on the host: the oracle's reference scores (oracle_np.exhaustive_scores:
+    CohereEnhancedVectorDB.py:283-293 / :302-318) of EVERY row for a few queries of the batch, their
+    (score desc, row asc) top-k, against the GPU's rows and scores -- both phases.  Row blocks run
+    on ``threads`` host threads (NumPy releases the GIL inside its kernels)."""
+    import concurrent.futures as cf
+    from oracle import oracle_np as O
+    t0 = time.perf_counter()
+    qs = [q for q in qsel if q < qf.shape[0]]
+    codes_h, x8_h, q_h = codes.cpu().numpy(), x8.cpu().numpy(), qf[qs].cpu().numpy()
+    n = codes_h.shape[0]
+    blk = 1 << 18
+    res = {}
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        for mode in ("binary", "int8_cosine"):
+            S = np.empty((len(qs), n), np.float64)
+
+            def part(a, mode=mode, S=S):
+                b = min(n, a + blk)
+                S[:, a:b] = O.exhaustive_scores(mode, q_h, codes=codes_h[a:b], x8=x8_h[a:b])
+            list(ex.map(part, range(0, n, blk)))
+            ref = O.exhaustive_topk(S, k)
+            m = {"binary": 2, "int8_cosine": 3}[mode]
+            g_rows = out[m][1][qs].cpu().numpy()
+            g_sc = out[m][2][qs].cpu().numpy()
+            res[mode] = {"rows_identical": bool(np.array_equal(g_rows, ref)),
+                         "scores_identical": bool(np.array_equal(g_sc, np.take_along_axis(S, ref, 1)))}
+    del codes_h, x8_h
+    return {"queries": qs, "rows": n, "k": k, "seconds": time.perf_counter() - t0, **res,
+            "checker": "oracle_np.exhaustive_scores over every row on the host (test infrastructure)"}
+
+
 def timed_loop(P, a, world, dev):
     for _ in range(a.warmup):
         P.step(False)
@@ -581,17 +619,98 @@ def run_c5(a, world, rank, dev):
         rs = min(m, 1_000_000)
         out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
                                               a.k, m, threads=cpu_threads(a))
+        out["cpu_gpu_identity"] = c5_identity(codes, x8, qf, P.final, a.k, cpu_threads(a))
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def launch_plan(gpus: int, env, device_count: int):
+    """How this process runs ``--gpus N`` (decided before any GPU call).
+
+    * ``("run", world, rank, local)``: this process is one rank -- either N = 1 without a
+      launcher, or one of the N ranks a launcher (torch.distributed.run, or this script's own
+      spawn) started with WORLD_SIZE = N.
+    * ``("spawn", N)``: N > 1 and no launcher: start N ranks of this script as child processes
+      (one per GPU) and exit with their status.
+    * ``("refuse", message)``: the launch cannot produce an N-GPU record (WORLD_SIZE != N, fewer
+      than N devices, a local rank without a device)."""
+    if gpus < 1:
+        return ("refuse", f"--gpus {gpus}: need at least 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if device_count < gpus:
+            return ("refuse", f"--gpus {gpus} but only {device_count} GPU(s) are visible")
+        if gpus == 1:
+            return ("run", 1, 0, 0)
+        return ("spawn", gpus)
+    world = int(ws)
+    if world != gpus:
+        return ("refuse", f"WORLD_SIZE={world} (launcher) but --gpus {gpus}: refusing to print a mislabelled record")
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", str(rank)))
+    if not (0 <= rank < world) or local < 0:
+        return ("refuse", f"bad RANK={rank} / LOCAL_RANK={local} for WORLD_SIZE={world}")
+    if local >= device_count:
+        return ("refuse", f"LOCAL_RANK={local} but only {device_count} GPU(s) are visible")
+    return ("run", world, rank, local)
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n ranks of this script (same argv) as child processes with the torch.distributed env
+    (127.0.0.1 rendezvous); rank 0's stdout is this process's stdout.  The parent never touches the
+    GPU.  If a rank fails, the others are terminated.  Returns the exit status."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"[launcher] rank {procs.index(p)} exited with {c}; stopping the other ranks")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --launch-probe (CPU tests of the launcher): pretend N devices, rendezvous over gloo, no GPU work
+    plan = launch_plan(a.gpus, os.environ, a.gpus if a.launch_probe else torch.cuda.device_count())
+    if plan[0] == "refuse":
+        log(f"bench.py: {plan[1]}")
+        sys.exit(2)
+    if plan[0] == "spawn":
+        sys.exit(spawn_ranks(plan[1]))
+    _, world, rank, local = plan
+    if a.launch_probe:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            t = torch.tensor([rank], dtype=torch.int64)
+            dist.all_reduce(t)
+            dist.destroy_process_group()
+            assert int(t) == world * (world - 1) // 2
+        if rank == 0:
+            print(json.dumps({"launch_probe": True, "n_gpus": world}), flush=True)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

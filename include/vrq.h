@@ -219,7 +219,12 @@ int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, vo
  * Exact for every input: int8-quantised queries on v_mfma_i32_32x32x32_i8 give scores within a
  * proven per-query bound, a sampled threshold keeps every row that can reach the top-k, and the
  * survivors are rescored exactly (heavy-tie inputs fall back to an exact scan of every row).
- * flags: 0, or a subset of the VRQ_GEMM_STAGE_* (issued in order = the full call).
+ * flags: 0, or a subset of the VRQ_GEMM_STAGE_* (issued in order SAMPLE, MAIN, FINISH on one
+ * workspace = the full call; FINISH consumes the thresholds SAMPLE wrote, so every MAIN + FINISH
+ * pair needs its own SAMPLE before it), optionally | VRQ_GEMM_NO_FALLBACK: queries the matrix
+ * path could not serve (heavy exact ties) are left with out_count = -1 and unwritten rows instead
+ * of taking the exact per-query scan of every row (callers that must bound latency; tests prove
+ * with it that the matrix path alone served a batch).
  * Supported: dim = 1024, 1 <= k <= 1024, 1 <= n < 2^32.
  * ------------------------------------------------------------------------- */
 #define VRQ_GEMM_BINARY 2
@@ -227,6 +232,7 @@ int vrq_int8_row_norms(const int8_t* x8, int64_t n, int32_t dim, double* out, vo
 #define VRQ_GEMM_STAGE_SAMPLE 16 /* query split + dense sample pass + per-query thresholds */
 #define VRQ_GEMM_STAGE_MAIN 32   /* thresholded pass over every row -> candidate lists */
 #define VRQ_GEMM_STAGE_FINISH 64 /* exact rescoring + sort of the candidates (+ exact fallback) */
+#define VRQ_GEMM_NO_FALLBACK 128 /* skip the exact fallback: unserved queries get out_count = -1 */
 size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k);
 /* int8 pieces per query of this build's matrix pass (1: q ~ S*a, 2: q ~ S*(a + b/256)); the
  * algorithmic ops of a pass are 2*nq*n*dim either way (for roofline reporting) */

@@ -101,3 +101,23 @@ def test_workspace_sizes_lane_extrema_samples():
 ])
 def test_argument_validation(call, expect):
     assert call(N.load()) == expect
+
+
+def test_release_library_ignores_tuning_environment(monkeypatch):
+    """The release libvrq.so plans from its defaults whatever the environment holds (it does not
+    even import getenv); the probe build libvrq_probe.so reads the VRQ_* tuning overrides."""
+    import subprocess
+    lib, probe = N.load(), N.load_probe()
+    nm = subprocess.run(["nm", "-D", N.lib_path()], capture_output=True, text=True).stdout
+    assert "getenv" not in nm
+    args = (3, 10_000_000, 1024, 1024, 10)
+    base = lib.vrq_gemm_topk_workspace_size(*args)
+    assert base == probe.vrq_gemm_topk_workspace_size(*args)
+    s3 = lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 100)
+    monkeypatch.setenv("VRQ_GEMM_CHUNK_MULT", "1")
+    monkeypatch.setenv("VRQ_GEMM_SAMPLE_DIV", "2")
+    monkeypatch.setenv("VRQ_SAMPLE_DIV", "4")
+    monkeypatch.setenv("VRQ_MFMA_MB", "4")
+    assert lib.vrq_gemm_topk_workspace_size(*args) == base
+    assert lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 100) == s3
+    assert probe.vrq_gemm_topk_workspace_size(*args) != base

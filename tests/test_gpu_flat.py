@@ -63,15 +63,15 @@ def _index(F, dev, batch=None):
     return idx
 
 
-def _search(idx, qf, k):
-    cnt, rows, sc = idx.search_rows(qf, k)
+def _search(idx, qf, k, flags=0):
+    cnt, rows, sc = idx.search_rows(qf, k, flags)
     torch.cuda.synchronize()
     return cnt.cpu().numpy(), rows.cpu().numpy(), sc.cpu().numpy()
 
 
 @pytest.mark.parametrize("k", [10, 100])
-def test_flat_ip_vs_oracle_matrix_path(dev, k, monkeypatch):
-    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")  # the matrix-core path alone must serve this batch
+def test_flat_ip_vs_oracle_matrix_path(dev, k):
+    from vectorragquantization_amd import _native as N
     rng = np.random.default_rng(21)
     n, nq = 70_000, 300
     F = _corpus(rng, n)
@@ -80,7 +80,7 @@ def test_flat_ip_vs_oracle_matrix_path(dev, k, monkeypatch):
     qf = _queries(rng, F, nq)
     qf[3] = F[123]
     idx = _index(F, dev, batch=20_000)            # bounds accumulate over several prepare batches
-    cnt, rows, sc = _search(idx, qf, k)
+    cnt, rows, sc = _search(idx, qf, k, N.VRQ_GEMM_NO_FALLBACK)  # the matrix-core path alone must serve it
     _check(F, qf, k, cnt, rows, sc)
 
 
@@ -178,15 +178,15 @@ def test_cohere_vector_db_float_surface(dev, tmp_path):
 
 
 @pytest.mark.parametrize("order", ["random", "cluster_sorted"])
-def test_flat_ip_1m_clustered_served_without_fallback(dev, monkeypatch, order):
+def test_flat_ip_1m_clustered_served_without_fallback(dev, order):
     """1M clustered rows (4096 clusters of ~244: the dense sample holds only a few rows of a query's
     cluster, so the sampled threshold admits far more rows than a candidate list holds).  The
     overflowing queries must be served by the retry pass (threshold raised to the k-th exact score
-    among the recorded candidates), not by the one-workgroup full-scan fallback: VRQ_GEMM_FALLBACK=0
+    among the recorded candidates), not by the one-workgroup full-scan fallback: VRQ_GEMM_NO_FALLBACK
     makes any fallback query an error.  Exact against a float64 matmul (ties within one f32 ulp).
     ``cluster_sorted`` stores the rows in cluster order (the sample's chunks then miss most clusters)."""
+    from vectorragquantization_amd import _native as N
     from vectorragquantization_amd.flat import flat_ip_prepare, flat_ip_topk
-    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")
     g = torch.Generator(device=dev).manual_seed(77)
     n, nq, k = 1_000_000, 128, 10
     cent = torch.randn((4096, 1024), generator=g, device=dev)
@@ -203,7 +203,7 @@ def test_flat_ip_1m_clustered_served_without_fallback(dev, monkeypatch, order):
     qf = (qf / qf.norm(dim=1, keepdim=True)).contiguous()
     bounds = torch.zeros((2,), dtype=torch.float64, device=dev)
     x8, inv = flat_ip_prepare(xf, bounds)
-    cnt, rows, sc = flat_ip_topk(xf, x8, inv, bounds, qf, k)
+    cnt, rows, sc = flat_ip_topk(xf, x8, inv, bounds, qf, k, flags=N.VRQ_GEMM_NO_FALLBACK)
     torch.cuda.synchronize()
     assert bool((cnt == k).all())
     S = (qf.double() @ xf.double().T).float().double()          # the f32-rounded exact dot

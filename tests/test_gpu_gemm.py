@@ -14,6 +14,8 @@ from oracle import oracle_np as O
 
 pytestmark = pytest.mark.gpu
 
+NOFB = 128  # VRQ_GEMM_NO_FALLBACK: an unserved query is an error (the matrix path alone must serve the batch)
+
 
 @pytest.fixture(scope="module")
 def dev():
@@ -39,13 +41,14 @@ def _queries(rng, F, nq):
     return (qf / np.linalg.norm(qf, axis=1, keepdims=True)).astype(np.float32)
 
 
-def _run(mode, qf, k, dev, codes=None, x8=None, row_offset=0, flags=0):
+def _run(mode, qf, k, dev, codes=None, x8=None, row_offset=0, flags=0, lib=None):
     from vectorragquantization_amd.enhanced import gemm_topk
     from vectorragquantization_amd.quant import int8_row_norms
     c_t = _t(codes, dev) if codes is not None else None
     x_t = _t(x8, dev) if x8 is not None else None
     nrm = int8_row_norms(x_t) if x_t is not None else None
-    cnt, rows, sc = gemm_topk(mode, _t(qf, dev), k, codes=c_t, x8=x_t, norms=nrm, row_offset=row_offset, flags=flags)
+    cnt, rows, sc = gemm_topk(mode, _t(qf, dev), k, codes=c_t, x8=x_t, norms=nrm, row_offset=row_offset, flags=flags,
+                              lib=lib)
     torch.cuda.synchronize()
     return cnt.cpu().numpy(), rows.cpu().numpy(), sc.cpu().numpy()
 
@@ -63,8 +66,7 @@ def _check(mode, qf, k, cnt, rows, sc, codes=None, x8=None, row_offset=0):
 
 
 @pytest.mark.parametrize("mode", ["binary", "int8_cosine"])
-def test_gemm_topk_vs_oracle(dev, mode, monkeypatch):
-    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")  # the matrix-core path alone must serve this batch
+def test_gemm_topk_vs_oracle(dev, mode):
     rng = np.random.default_rng(5)
     n, nq, k = 70_000, 200, 10                    # > the 32768-row sample; two query blocks + padding
     F = _corpus(rng, n)
@@ -73,20 +75,19 @@ def test_gemm_topk_vs_oracle(dev, mode, monkeypatch):
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = _queries(rng, F, nq)
     qf[7] = F[123]                                # a query whose top rows are the tied duplicates
-    cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, row_offset=1000)
+    cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, row_offset=1000, flags=NOFB)  # matrix path alone
     _check(mode, qf, k, cnt, rows, sc, codes=codes, x8=x8, row_offset=1000)
 
 
 @pytest.mark.parametrize("k", [1, 100])
-def test_gemm_topk_k_range(dev, k, monkeypatch):
-    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")
+def test_gemm_topk_k_range(dev, k):
     rng = np.random.default_rng(11 + k)
     n, nq = 40_000, 130
     F = _corpus(rng, n, 16)
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = _queries(rng, F, nq)
     for mode in ("binary", "int8_cosine"):
-        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8)
+        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, flags=NOFB)
         _check(mode, qf, k, cnt, rows, sc, codes=codes, x8=x8)
 
 
@@ -147,15 +148,18 @@ def test_gemm_topk_stage_split(dev):
 
 
 def test_gemm_topk_many_candidates(dev, monkeypatch):
-    """A small sample (VRQ_GEMM_SAMPLE_DIV) and k = 100 leave thousands of candidates per query: the
-    finish kernel's running top-k walks them in several batches; the fallback stays off."""
-    monkeypatch.setenv("VRQ_GEMM_FALLBACK", "0")
+    """A small sample (VRQ_GEMM_SAMPLE_DIV, read only by the probe build libvrq_probe.so) and k = 100
+    leave thousands of candidates per query: the finish kernel's running top-k walks them in several
+    batches; the fallback stays off."""
+    from vectorragquantization_amd import _native as N
     monkeypatch.setenv("VRQ_GEMM_SAMPLE_DIV", "8")
+    probe = N.load_probe()
     rng = np.random.default_rng(17)
     n, nq, k = 200_000, 40, 100
     F = _corpus(rng, n, 32)
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = _queries(rng, F, nq)
     for mode in ("binary", "int8_cosine"):
-        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8)
+        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, flags=NOFB, lib=probe)
         _check(mode, qf, k, cnt, rows, sc, codes=codes, x8=x8)
+

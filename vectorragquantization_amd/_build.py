@@ -15,6 +15,9 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvrq.so")
+# the probe build: the same sources with -DVRQ_TUNING_ENV, whose planners read the VRQ_* tuning
+# overrides from the environment (tools/ sweeps and one test); the release libvrq.so never does
+PROBE_LIB = os.path.join(PKG, "libvrq_probe.so")
 OBJDIR = os.path.join(PKG, "_obj")
 SOURCES = ["hamming_scan.hip", "hamming_mfma.hip", "select_rescore.hip", "encode.hip", "gemm_topk.hip", "dequant.hip"]
 ARCH = os.environ.get("VRQ_OFFLOAD_ARCH", "gfx950")
@@ -38,22 +41,27 @@ def _deps() -> list:
         os.path.join(os.path.dirname(PKG), "include", "vrq.h")]
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+def up_to_date(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return False
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return all(os.path.getmtime(d) <= t for d in _deps())
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+    """Build libvrq.so and libvrq_probe.so (whichever is stale); returns the release library path."""
+    todo = [(lib, probe) for lib, probe in ((LIB, False), (PROBE_LIB, True)) if force or not up_to_date(lib)]
+    if not todo:
         return LIB
     hipcc = _hipcc()
-    os.makedirs(OBJDIR, exist_ok=True)
 
-    def compile_one(src):
-        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc, *CFLAGS, *EXTRA.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj]
+    def compile_one(job):
+        src, probe = job
+        odir = os.path.join(OBJDIR, "probe") if probe else OBJDIR
+        os.makedirs(odir, exist_ok=True)
+        obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc, *CFLAGS, *(["-DVRQ_TUNING_ENV"] if probe else []), *EXTRA.get(src, []), "-c",
+               os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -61,14 +69,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(r.stderr, file=sys.stderr)
         return obj
 
-    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp],
-                       capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link of libvrq.so failed:\n{r.stderr}")
-    os.replace(tmp, LIB)
+    jobs = [(src, probe) for _, probe in todo for src in SOURCES]
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(compile_one, jobs))
+    for i, (lib, _) in enumerate(todo):
+        tmp = lib + ".tmp"
+        r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC",
+                            *objs[i * len(SOURCES):(i + 1) * len(SOURCES)], "-o", tmp], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link of {os.path.basename(lib)} failed:\n{r.stderr}")
+        os.replace(tmp, lib)
     return LIB
 
 

@@ -32,6 +32,7 @@ VRQ_GEMM_FLOAT_IP = 4
 VRQ_GEMM_STAGE_SAMPLE = 16
 VRQ_GEMM_STAGE_MAIN = 32
 VRQ_GEMM_STAGE_FINISH = 64
+VRQ_GEMM_NO_FALLBACK = 128
 VRQ_RESCORE_F32 = 16  # vrq_rescore_dequant: compare_float32 rows
 VRQ_SCAN_KIND_VALU = 0
 VRQ_SCAN_KIND_MFMA = 1
@@ -89,33 +90,49 @@ def lib_path() -> str:
     return os.environ.get("VRQ_LIB", _build.LIB)
 
 
+def _open(path: str, default: str):
+    if not os.path.exists(path) or (path == default and not _build.up_to_date(default)):
+        try:
+            _build.build()
+        except Exception as e:  # no hipcc on this host and no prebuilt library
+            if not os.path.exists(path):
+                raise VrqNativeError(f"{os.path.basename(path)} missing and cannot be built: {e}") from e
+    try:
+        lib = C.CDLL(path)
+    except OSError as e:
+        raise VrqNativeError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.vrq_abi_version() != 1:
+        raise VrqNativeError("libvrq ABI version mismatch")
+    return lib
+
+
 def load():
     """Load (building first if needed and possible) libvrq.so; raise on failure."""
     global _lib
     if _lib is not None:
         return _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        path = lib_path()
-        if not os.path.exists(path) or (path == _build.LIB and not _build.up_to_date()):
-            try:
-                _build.build()
-            except Exception as e:  # no hipcc on this host and no prebuilt library
-                if not os.path.exists(path):
-                    raise VrqNativeError(f"libvrq.so missing and cannot be built: {e}") from e
-        try:
-            lib = C.CDLL(path)
-        except OSError as e:
-            raise VrqNativeError(f"cannot load {path}: {e}") from e
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        if lib.vrq_abi_version() != 1:
-            raise VrqNativeError("libvrq ABI version mismatch")
-        _lib = lib
-        return lib
+        if _lib is None:
+            _lib = _open(lib_path(), _build.LIB)
+        return _lib
+
+
+_probe = None
+
+
+def load_probe():
+    """The probe build libvrq_probe.so: the same kernels, but its planners read the VRQ_* tuning
+    overrides (VRQ_SAMPLE_DIV, VRQ_MFMA_MB, VRQ_MFMA_ROWS, VRQ_GEMM_SAMPLE_DIV, VRQ_GEMM_CHUNK_MULT)
+    from the environment.  For sweeps and tests only; the product path always uses load()."""
+    global _probe
+    with _lock:
+        if _probe is None:
+            _probe = _open(_build.PROBE_LIB, _build.PROBE_LIB)
+        return _probe
 
 
 def check(rc: int, what: str) -> None:

@@ -90,6 +90,9 @@ constexpr int T3N = T3 + GRT * 8;    // ... + their 32 f64 norms
 constexpr int T2 = GRT * 128;        // Phase-II packed tile (4 KiB)
 constexpr int U2 = GKS * 1024;       // Phase-II unpacked tile [k-step][lane][16 B] (32 KiB)
 
+// main-pass chunks per (CU, query block): 4 keeps the query blocks that stream the same chunk
+// within L2 reach of each other (PMC bytes 1.1x algorithmic vs 1.9x at 1, equal time; round 2)
+constexpr int kChunkMult = 4;
 constexpr int FB_BATCH = 1024;       // rows per batch of the exact fallback
 constexpr int KMAX5 = 1024;          // k bound of the path
 constexpr int64_t kMinSample = 32768;
@@ -923,12 +926,21 @@ __global__ __launch_bounds__(256) void gemm_fallback_kernel(const Rows c, int64_
                                                             int32_t* __restrict__ out_count,
                                                             int64_t* __restrict__ out_rows,
                                                             double* __restrict__ out_scores,
-                                                            const int32_t* __restrict__ fb_flag) {
+                                                            const int32_t* __restrict__ fb_flag,
+                                                            bool skip) {
   __shared__ uint64_t key[KMAX5 + FB_BATCH];
   __shared__ uint32_t row[KMAX5 + FB_BATCH];
   __shared__ int32_t fill;
   const int q = blockIdx.x, tid = threadIdx.x;
   if (fb_flag[q] != 1) return;
+  if (skip) {  // VRQ_GEMM_NO_FALLBACK: report the query as unserved
+    for (int i = tid; i < k; i += 256) {
+      out_rows[(int64_t)q * k + i] = -1;
+      out_scores[(int64_t)q * k + i] = __builtin_nan("");
+    }
+    if (tid == 0) out_count[q] = -1;
+    return;
+  }
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
   const int kc =
@@ -955,16 +967,16 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   if (n < 1 || n >= (int64_t(1) << 32) || nq < 1 || k < 1 || k > KMAX5) return VRQ_EUNSUPPORTED;
   p->nqb = (nq + GQB - 1) / GQB;
   p->nq_pad = p->nqb * GQB;
-  // chunks per query block: one WG per CU (x VRQ_GEMM_CHUNK_MULT, a tuning override: shorter chunks
-  // keep the query blocks that share a chunk closer in time, so they share its L2 lines)
-  const char* cm = getenv("VRQ_GEMM_CHUNK_MULT");
-  const int mult = cm && atoi(cm) >= 1 ? atoi(cm) : 1;
+  // chunks per query block: kChunkMult per CU (VRQ_GEMM_CHUNK_MULT in the probe build): shorter
+  // chunks keep the query blocks that share a chunk closer in time, so they share its L2 lines
+  const int cm = tuning_int("VRQ_GEMM_CHUNK_MULT", kChunkMult);
+  const int mult = cm >= 1 ? cm : kChunkMult;
   const int want = (256 / p->nqb > 0 ? 256 / p->nqb : 1) * mult;
   // sample rows: the sampled threshold alone admits ~k * n / S rows per query; aim at FIN_CAP /
   // CAP_MULT so that the margin's extra rows still fit (VRQ_GEMM_SAMPLE_DIV overrides n / S)
   int64_t S = (int64_t)((double)CAP_MULT * (double)k * (double)n / (double)FIN_CAP);
-  const char* ev = getenv("VRQ_GEMM_SAMPLE_DIV");
-  if (ev && atoi(ev) >= 1) S = n / atoi(ev);
+  const int ev = tuning_int("VRQ_GEMM_SAMPLE_DIV", 0);
+  if (ev >= 1) S = n / ev;
   if (S < kMinSample) S = kMinSample;
   if (S > kMaxSample) S = kMaxSample;
   if (S > n) S = n;
@@ -1092,9 +1104,8 @@ void launch_finish(const Rows& c, const uint8_t* src, int64_t n, int64_t row_off
   hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
                      (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
                      flag, thr, alpha, beta, delta, qbf);
-  if (fb)
-    hipLaunchKernelGGL(gemm_fallback_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, out_count,
-                       out_rows, out_scores, (const int32_t*)flag);
+  hipLaunchKernelGGL(gemm_fallback_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, out_count,
+                     out_rows, out_scores, (const int32_t*)flag, !fb);
 }
 
 // The three stages shared by every mode.  The matrix passes of VRQ_GEMM_FLOAT_IP are the int8
@@ -1155,10 +1166,8 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
     VRQ_LAUNCH_CHECK();
   }
   if (st & VRQ_GEMM_STAGE_FINISH) {
-    // VRQ_GEMM_FALLBACK=0 (tests only, read per call): skip the exact fallback, leaving flagged
-    // queries' outputs unwritten, to prove the matrix-core path alone served a batch
-    const char* fe = getenv("VRQ_GEMM_FALLBACK");
-    const bool fb = !(fe && fe[0] == '0');
+    // VRQ_GEMM_NO_FALLBACK: the flagged queries get out_count = -1 instead of the exact scan
+    const bool fb = !(flags & VRQ_GEMM_NO_FALLBACK);
     const int8_t* qac = qa;
     const double *al = alpha, *be = beta, *de = delta;
     if (mode == VRQ_GEMM_INT8_COSINE)

@@ -1323,15 +1323,14 @@ static int sample_order(double lam, int K) {
 
 int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   if (nq < 1 || K < 1 || K > kMfmaMaxK) return VRQ_EUNSUPPORTED;
-  // VRQ_MFMA_MB: tuning override of the M-blocks per wave (2 or 4; read per call, no state)
-  const char* em = getenv("VRQ_MFMA_MB");
-  p->mb = em && (atoi(em) == 2 || atoi(em) == 4) ? atoi(em) : nq >= kMbLargeMinQueries ? kMbLarge : kMbSmall;
+  // VRQ_MFMA_MB: probe-build override of the M-blocks per wave (2 or 4)
+  const int em = tuning_int("VRQ_MFMA_MB", 0);
+  p->mb = (em == 2 || em == 4) ? em : nq >= kMbLargeMinQueries ? kMbLarge : kMbSmall;
   p->qpb = p->mb == kMbLarge ? MfmaShape<kMbLarge>::QPB : MfmaShape<kMbSmall>::QPB;
   p->nqb = (nq + p->qpb - 1) / p->qpb;
   // small batches (nq <= 128): the row-split kernel K1r, all queries in every wave
-  // (VRQ_MFMA_ROWS=0/1: tuning override, read per call)
-  const char* er = getenv("VRQ_MFMA_ROWS");
-  p->rows = nq <= kRowsMaxQueries && !(er && er[0] == '0');
+  // (VRQ_MFMA_ROWS=0: probe-build override)
+  p->rows = nq <= kRowsMaxQueries && tuning_int("VRQ_MFMA_ROWS", 1) != 0;
   if (p->rows) {
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
@@ -1343,9 +1342,9 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   // robust to corpora stored in cluster order), in nsc chunks (one workgroup per CU and query block)
   // of T tiles: tile i = c*T + t starts at row i * ts, the last one inside [0, n).  S = n/32, at least
   // kMfmaMinSample and at most kMfmaMaxSample rows (the dense pass and its selection cost O(nq S)).
-  // VRQ_SAMPLE_DIV: tuning override of the sample fraction (read per call, no state)
-  const char* ev = getenv("VRQ_SAMPLE_DIV");
-  const int64_t div = ev && atoi(ev) >= 2 ? atoi(ev) : kMfmaSampleDiv;
+  // VRQ_SAMPLE_DIV: probe-build override of the sample fraction
+  const int64_t ev = tuning_int("VRQ_SAMPLE_DIV", 0);
+  const int64_t div = ev >= 2 ? ev : kMfmaSampleDiv;
   int64_t S = n / div;
   if (S > kMfmaMaxSample) S = kMfmaMaxSample;
   if (S < kMfmaMinSample) S = kMfmaMinSample;

@@ -27,6 +27,21 @@ constexpr int32_t DIST_NONE = 0x7fffffff;
     }                                                    \
   } while (0)
 
+// Planning overrides for sweeps.  Only the probe build (libvrq_probe.so, compiled with
+// -DVRQ_TUNING_ENV for tools/ and one test) reads them from the environment; the release
+// libvrq.so always plans with the defaults, whatever the environment holds.
+#ifdef VRQ_TUNING_ENV
+}  // namespace vrq
+#include <stdlib.h>
+namespace vrq {
+inline int tuning_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+#else
+inline int tuning_int(const char*, int dflt) { return dflt; }
+#endif
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {

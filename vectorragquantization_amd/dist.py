@@ -62,11 +62,15 @@ def unpack_candidates(buf: torch.Tensor, S: int, nq: int, K: int):
 
 
 def gather_candidates(local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather the packed buffers of every rank (single collective)."""
+    """All-gather the packed buffers of every rank (single collective).  With the ``nccl`` backend
+    (RCCL) device buffers travel GPU to GPU; a ``gloo`` group (CPU tests, several ranks sharing one
+    GPU) stages the device buffer through host memory."""
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.numel(),), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, local, group=group)
-    return out
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    src = local.cpu() if stage else local
+    out = torch.empty((world * src.numel(),), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.to(local.device) if stage else out
 
 
 def merge_shards(cnt, rows, d, s2, s3, k: int, K3: int):

@@ -62,12 +62,13 @@ class SearchBatch:
 
 def gemm_topk(mode: str, qf: torch.Tensor, k: int, codes: torch.Tensor | None = None,
               x8: torch.Tensor | None = None, norms: torch.Tensor | None = None, row_offset: int = 0,
-              flags: int = 0, workspace: torch.Tensor | None = None):
+              flags: int = 0, workspace: torch.Tensor | None = None, lib=None):
     """Exhaustive Phase-II (``mode="binary"``) or Phase-III (``mode="int8_cosine"``) top-k of a query
     batch over EVERY row on the matrix cores (``vrq_gemm_topk``, BASELINE config 5): the scores of
     ``CohereEnhancedVectorDB.py:283-293`` / ``:302-318`` ordered like the reference's stable
     ``sorted(..., reverse=True)`` over rows in index order.  Returns (count i32[nq], rows i64[nq, k],
-    scores f64[nq, k]) device tensors."""
+    scores f64[nq, k]) device tensors.  ``flags``: VRQ_GEMM_STAGE_* / VRQ_GEMM_NO_FALLBACK; ``lib``:
+    another build of the library (the probe build, for sweeps), default libvrq.so."""
     m = {"binary": N.VRQ_GEMM_BINARY, "int8_cosine": N.VRQ_GEMM_INT8_COSINE}[mode]
     src = codes if m == N.VRQ_GEMM_BINARY else x8
     dev = qf.device
@@ -75,7 +76,7 @@ def gemm_topk(mode: str, qf: torch.Tensor, k: int, codes: torch.Tensor | None = 
     cnt = torch.full((nq,), -2, dtype=torch.int32, device=dev)  # -2: never written
     rows = torch.full((nq, k), -2, dtype=torch.int64, device=dev)
     scores = torch.empty((nq, k), dtype=torch.float64, device=dev)
-    lib = N.load()
+    lib = lib or N.load()
     need = lib.vrq_gemm_topk_workspace_size(m, n, qf.shape[1], nq, k)
     if need == 0:
         raise N.VrqNativeError(f"vrq_gemm_topk: unsupported shape n={n} dim={qf.shape[1]} nq={nq} k={k}")
@@ -84,9 +85,10 @@ def gemm_topk(mode: str, qf: torch.Tensor, k: int, codes: torch.Tensor | None = 
     N.check(lib.vrq_gemm_topk(m, N.ptr(codes), N.ptr(x8), N.ptr(norms), n, qf.shape[1], row_offset, N.ptr(qf), nq,
                               k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores), N.ptr(workspace),
                               workspace.numel(), N.stream_handle(dev)), "vrq_gemm_topk")
-    if os.environ.get("VRQ_GEMM_FALLBACK") == "0" and bool((cnt < 0).any()):
-        # test hook: the library skipped the exact fallback and left the flagged queries unwritten
-        raise N.VrqNativeError("vrq_gemm_topk: queries needed the exact fallback, which VRQ_GEMM_FALLBACK=0 disabled")
+    if bool((cnt < 0).any()):
+        # only with VRQ_GEMM_NO_FALLBACK in flags: the library left queries it could not serve on the
+        # matrix path unwritten (count -1) instead of running the exact scan
+        raise N.VrqNativeError("vrq_gemm_topk: queries needed the exact fallback, which VRQ_GEMM_NO_FALLBACK disabled")
     return cnt, rows, scores
 
 

@@ -62,9 +62,10 @@ def flat_ip_topk(xf: torch.Tensor, x8: torch.Tensor, inv_scale: torch.Tensor, bo
     N.check(lib.vrq_flat_ip_topk(N.ptr(xf), N.ptr(x8), N.ptr(inv_scale), N.ptr(bounds), n, qf.shape[1], row_offset,
                                  N.ptr(qf), nq, k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores),
                                  N.ptr(workspace), workspace.numel(), N.stream_handle(dev)), "vrq_flat_ip_topk")
-    if os.environ.get("VRQ_GEMM_FALLBACK") == "0" and bool((cnt < 0).any()):
-        # test hook: the library skipped the exact fallback and left the flagged queries unwritten
-        raise N.VrqNativeError("vrq_flat_ip_topk: queries needed the exact fallback, which VRQ_GEMM_FALLBACK=0 disabled")
+    if bool((cnt < 0).any()):
+        # only with VRQ_GEMM_NO_FALLBACK in flags: the library left queries it could not serve on the
+        # matrix path unwritten (count -1) instead of running the exact scan
+        raise N.VrqNativeError("vrq_flat_ip_topk: queries needed the exact fallback, which VRQ_GEMM_NO_FALLBACK disabled")
     return cnt, rows, scores
 
 
@@ -137,8 +138,9 @@ class FloatIndexIDMap:
         self._inv.append(inv)
         self._ids.append(ids_t)
 
-    def search_rows(self, qf, k: int):
-        """Device (count, rows, scores) of the exact top-k (internal rows)."""
+    def search_rows(self, qf, k: int, flags: int = 0):
+        """Device (count, rows, scores) of the exact top-k (internal rows); ``flags`` as
+        ``vrq_flat_ip_topk`` (e.g. VRQ_GEMM_NO_FALLBACK)."""
         qf = as_device_tensor(qf, torch.float32, self.device).reshape(-1, self.d)
         lib = N.load()
         need = lib.vrq_gemm_topk_workspace_size(N.VRQ_GEMM_FLOAT_IP, self.ntotal, self.d, qf.shape[0], k)
@@ -146,7 +148,7 @@ class FloatIndexIDMap:
             self._ws = torch.empty((max(need, 8),), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
             return flat_ip_topk(self._xf.view(), self._x8.view(), self._inv.view(), self.bounds, qf, k,
-                                workspace=self._ws)
+                                flags=flags, workspace=self._ws)
 
     def search(self, q, k: int):
         """FAISS ``search``: numpy (distances f32[nq, k], labels i64[nq, k]); unused slots -FLT_MAX / -1."""
@@ -161,8 +163,6 @@ class FloatIndexIDMap:
         r = rows.cpu().numpy()
         s = scores.cpu().numpy()
         ids = self.id_map.cpu().numpy()
-        if (cnt < 0).any():  # only when the VRQ_GEMM_FALLBACK=0 test hook skipped a query's fallback
-            raise N.VrqNativeError("FloatIndexIDMap.search: a query was left unserved (exact fallback disabled)")
         for j in range(nq):
             c = int(cnt[j])
             D[j, :c] = s[j, :c].astype(np.float32)
