@@ -130,10 +130,53 @@ def test_safe_unpickle_values_and_refusals():
 def test_rocksdict_scalar_encodings():
     assert D.decode_rocksdict(b"\x02abc") == "abc"
     assert D.decode_rocksdict(b"\x01\x00\xff") == b"\x00\xff"
-    assert D.decode_rocksdict(b"\x03" + (-7).to_bytes(8, "little", signed=True)) == -7
-    assert D.decode_rocksdict(b"\x04" + struct.pack("<d", 1.5)) == 1.5
-    with pytest.raises(D.DocStoreError):
-        D.decode_rocksdict(b"\x7f")
+    # int / float payloads: byte order pinned by no reference artefact -> refused, never guessed
+    for bad in (b"\x7f", b"\x03" + (-7).to_bytes(8, "little", signed=True), b"\x04" + struct.pack("<d", 1.5)):
+        with pytest.raises(D.DocStoreError):
+            D.decode_rocksdict(bad)
+
+
+def _vi(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append(n & 0x7F | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def test_write_batch_column_family_records():
+    """RocksDB ValueType tags: 0x4 CF deletion, 0x5 CF value, 0x8 CF single deletion carry a family
+    id; other families' records are consumed (their payload and sequence number) but not returned;
+    LogData / Noop carry no sequence number; range deletions and merges are refused."""
+    k, v = _rd_key("7"), _rd_pickle({"doc": "x"})
+    rec = b"".join([
+        b"\x05" + _vi(3) + _vi(len(k)) + k + _vi(len(v)) + v,   # CF 3 put of the same key: not ours
+        b"\x03" + _vi(4) + b"blob",                              # LogData: no sequence number
+        b"\x05" + _vi(0) + _vi(len(k)) + k + _vi(len(v)) + v,   # default-CF put via the CF form
+        b"\x04" + _vi(3) + _vi(len(k)) + k,                      # CF 3 delete
+        b"\x0d",                                                 # Noop
+        b"\x08" + _vi(0) + _vi(len(k)) + k,                      # default-CF single deletion
+        b"\x01" + _vi(len(k)) + k + _vi(len(v)) + v,            # plain put
+    ])
+    w = struct.pack("<QI", 100, 5) + rec
+    out = list(D._write_batch(w))
+    assert [(key, seq, typ) for key, seq, typ, _ in out] == [(k, 101, 1), (k, 103, 0), (k, 104, 1)]
+    assert out[0][3] == v and out[2][3] == v
+    for tag in (b"\x0f", b"\x0e" + _vi(0), b"\x02"):
+        with pytest.raises(D.DocStoreError):
+            list(D._write_batch(struct.pack("<QI", 1, 1) + tag + _vi(len(k)) + k + _vi(1) + b"z"))
+
+
+def test_safe_unpickle_protocol5_arrays():
+    x = np.arange(-6, 6, dtype=np.int8).reshape(3, 4)
+    f = np.asfortranarray(np.arange(6, dtype="<f4").reshape(2, 3))
+    out = D.safe_unpickle(pickle.dumps({"int8": x, "f": f, "doc": "d"}, protocol=5))
+    assert np.array_equal(out["int8"], x) and out["int8"].dtype == np.int8
+    assert np.array_equal(out["f"], f) and out["doc"] == "d"
+    bufs = []
+    with pytest.raises(D.DocStoreError):  # out-of-band buffers (NEXT_BUFFER) are refused
+        D.safe_unpickle(pickle.dumps(x, protocol=5, buffer_callback=bufs.append))
 
 
 def test_search3_refuses_inconsistent_rows():

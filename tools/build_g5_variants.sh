@@ -8,7 +8,7 @@ OBJ=vectorragquantization_amd/_obj
 mkdir -p tools/probes/g5
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 -DVRQ_TUNING_ENV \
     $flags -c vectorragquantization_amd/csrc/gemm_topk.hip -o tools/probes/g5/gemm_$name.o &
 done
 wait

@@ -63,6 +63,14 @@
 #ifndef VRQ_G5_NORM_REG
 #define VRQ_G5_NORM_REG 0  // Phase III: the tile's norms by a plain global load into registers (1) instead of LDS-DMA
 #endif
+#ifndef VRQ_G5_UREC
+#define VRQ_G5_UREC 1  // thresholded pass: flush recomputes u from the still-live accumulators (no ures[] file)
+#endif
+// timing-only probes of the DMA's cost (wrong results): 1 = every tile's DMA reads the chunk's first
+// tile (L2-resident source), 2 = the pieces are plain global loads into a discarded register (no LDS write)
+#ifndef VRQ_G5_DMA_PROBE
+#define VRQ_G5_DMA_PROBE 0
+#endif
 
 namespace vrq {
 namespace g5 {
@@ -293,7 +301,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     uint8_t* lds;
   };
   auto dma_tile = [&](int t, int slot_i) {  // whole tiles (not tiny)
-    const int64_t tr0 = row0 + tstart(t);
+    const int64_t tr0 = row0 + (VRQ_G5_DMA_PROBE == 1 ? 0 : tstart(t));
     DmaTile d;
     d.gsrc = src + (tr0 + 8 * w) * RB;
     d.gnrm = reinterpret_cast<const uint8_t*>(norms + tr0);
@@ -310,7 +318,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     }
     const uint8_t* g = d.gsrc + loff[P3 ? i : 0];
     uint8_t* ld = d.lds + (P3 ? (8 * w + i) * 1024 : w * 1024);
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
+    if constexpr (VRQ_G5_DMA_PROBE == 2) {
+      v4i sink;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sink) : "v"(g) : "memory");
+      asm volatile("" ::"v"(sink));
+    } else {
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
+    }
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
     if (P3 && i == 8) {
@@ -396,12 +410,16 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   if (!DENSE && l < GQW) lcnt[w * GQW + l] = 0;  // made visible by the first tile's barrier
   v16i acc[2][2];        // [tile parity][piece]
   // results of the previous tile (flushed at the top of the next-but-one tile): the sample pass
-  // keeps u; the thresholded pass keeps u - thr (a hit iff >= 0; NaN never) and their running max
-  float ures[NE];
-  float umax = -__builtin_inff();
+  // keeps u; the thresholded pass keeps u - thr (a hit iff >= 0; NaN never) and their running max.
+  // UREC: the thresholded pass keeps only the running max; the rare flush of a wave with a hit
+  // recomputes u - thr from the tile's accumulators, which stay live until the next-but-one tile's
+  // first MFMA (32 VGPRs fewer than a ures[] file)
+  constexpr bool UREC = !DENSE && VRQ_G5_UREC;
+  float ures[UREC ? 1 : NE];
+  float umax = -__builtin_inff(), uodd = 0.f;
 #pragma unroll
-  for (int e = 0; e < NE; ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
-  float invc = 0.f, invp = 0.f;  // Phase III 1/||x|| (NaN: zero norm or past the chunk)
+  for (int e = 0; e < (UREC ? 1 : NE); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
+  float invc = 0.f, invp = 0.f, invpp = 0.f;  // Phase III 1/||x|| of tiles t, t-1, t-2 (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
 
@@ -415,8 +433,9 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     else
       return P3 ? fmaf(u, inv, -th[e]) : u - th[e];
   };
-  // results of tile tt (computed in the following tile's shadow) -> HBM
-  auto flush = [&](int tt) {
+  // results of tile tt (computed in the following tile's shadow) -> HBM; (a0, a1, inv): tile tt's
+  // accumulators and 1/||x|| (UREC)
+  auto flush = [&](int tt, const v16i& a0, const v16i& a1, float inv) {
     const int lr = tstart(tt) + r;
     const bool ok = lane_valid(tt);
     if constexpr (!DENSE) {
@@ -424,7 +443,10 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         uint32_t m = 0;
         static_for<0, NE>([&](auto E) {
           constexpr int e = decltype(E)::value;
-          m |= (ures[e] >= 0.f ? 1u : 0u) << e;
+          if constexpr (UREC)
+            m |= (uval(a0, a1, e, inv) >= 0.f ? 1u : 0u) << e;
+          else
+            m |= (ures[e] >= 0.f ? 1u : 0u) << e;
         });
         if (!ok) m = 0;
         while (m) {
@@ -446,9 +468,14 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   auto test = [&](float u, int e, bool vp) {
     if constexpr (DENSE) {
       ures[e] = fmaxf(ures[e], vp ? u : __builtin_nanf(""));
+    } else if constexpr (UREC) {
+      if (e & 1)
+        umax = fmaxf(umax, fmaxf(uodd, u));  // pairs fold into one v_max3
+      else
+        uodd = u;
     } else {
       ures[e] = u;
-      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));  // pairs fold into one v_max3
+      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));
     }
   };
 
@@ -480,7 +507,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         wait_vm<0>();
     }
     if (!(VRQ_G5_BISECT & 4)) barrier_all();
-    if (!DENSE && t >= 2) flush(t - 2);
+    if (!DENSE && t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);  // tile t-2's accumulators: acc[p] until this tile's first MFMA
     const bool vprev = DENSE ? lane_valid(t - 1) : true;  // (the sample pass's test of tile t-1)
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
     const bool dma = t + AHEAD < ntiles;
@@ -557,6 +584,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       }
       VRQ_SCHED_FENCE();
     });
+    invpp = invp;
     invp = invc;
     sl = sl1;
   };
@@ -573,8 +601,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   if (t < ntiles) tile(I1{}, NOTFIRST{}, t);
   wait_vm<0>();
   // tile ntiles-2 (tested during the last tile), then the last tile itself
-  if (!DENSE && ntiles >= 2) flush(ntiles - 2);
   const int pl = (ntiles - 1) & 1;
+  if (!DENSE && ntiles >= 2) {
+    if (pl)
+      flush(ntiles - 2, acc[0][0], acc[0][1], invpp);
+    else
+      flush(ntiles - 2, acc[1][0], acc[1][1], invpp);
+  }
   const bool vlast = lane_valid(ntiles - 1);
 #pragma unroll
   for (int e = 0; e < NE; ++e)
@@ -585,8 +618,10 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       const int q = qbase + qrow(e);
       if (q < nq) dv[(int64_t)q * dv_stride + (int64_t)chunk * GRT + r] = ures[e];
     }
+  } else if (pl) {
+    flush(ntiles - 1, acc[1][0], acc[1][1], invp);
   } else {
-    flush(ntiles - 1);
+    flush(ntiles - 1, acc[0][0], acc[0][1], invp);
   }
   if constexpr (!DENSE) {
     wait_lgkm0();

@@ -25,11 +25,14 @@ from __future__ import annotations
 
 import glob
 import io
+import logging
 import os
 import pickletools
 import struct
 
 import numpy as np
+
+logger = logging.getLogger(__name__)
 
 
 class DocStoreError(RuntimeError):
@@ -243,26 +246,51 @@ def read_wal(path: str):
         yield from _write_batch(bytes(rec))
 
 
+# WriteBatch record tags (RocksDB dbformat.h ValueType)
+_WB_DEL, _WB_PUT, _WB_MERGE, _WB_LOGDATA = 0x0, 0x1, 0x2, 0x3
+_WB_CF_DEL, _WB_CF_PUT, _WB_CF_MERGE, _WB_SDEL, _WB_CF_SDEL = 0x4, 0x5, 0x6, 0x7, 0x8
+_WB_NOOP, _WB_CF_RANGE_DEL, _WB_RANGE_DEL = 0xD, 0xE, 0xF
+_WB_CF = {_WB_CF_DEL: _WB_DEL, _WB_CF_PUT: _WB_PUT, _WB_CF_SDEL: _WB_SDEL, _WB_CF_MERGE: _WB_MERGE,
+          _WB_CF_RANGE_DEL: _WB_RANGE_DEL}
+
+
 def _write_batch(w: bytes):
+    """Yield (user_key, seq, type, value) of the default column family's Puts / Deletes of one
+    WriteBatch.  Records of other column families consume their payload and sequence number but
+    are not returned (rocksdict stores everything in the default family); LogData and Noop records
+    carry no sequence number; merges and range deletions are refused (rocksdict issues neither)."""
     seq, count = struct.unpack_from("<QI", w, 0)
-    p = 12
-    for i in range(count):
+    p, i = 12, 0
+    while i < count:
+        if p >= len(w):
+            raise DocStoreError("WriteBatch shorter than its record count")
         tag = w[p]
         p += 1
-        if tag in (4, 5, 0xE):  # column-family variants: skip the family id (only default is used)
-            _, p = _varint(w, p)
-            tag = {4: 1, 5: 0, 0xE: 7}[tag]
+        if tag == _WB_LOGDATA:          # a blob for the log only: no key, no sequence number
+            bl, p = _varint(w, p)
+            p += bl
+            continue
+        if tag == _WB_NOOP:
+            continue
+        cf = 0
+        if tag in _WB_CF:
+            cf, p = _varint(w, p)
+            tag = _WB_CF[tag]
+        if tag in (_WB_MERGE, _WB_RANGE_DEL):
+            raise DocStoreError(f"unsupported WriteBatch record type {tag:#x} (merge / range deletion)")
+        if tag not in (_WB_PUT, _WB_DEL, _WB_SDEL):
+            raise DocStoreError(f"unsupported WriteBatch record type {tag:#x}")
         kl, p = _varint(w, p)
         key = w[p:p + kl]
         p += kl
-        if tag == 1:        # kTypeValue
+        val = b""
+        if tag == _WB_PUT:
             vl, p = _varint(w, p)
-            yield key, seq + i, 1, w[p:p + vl]
+            val = w[p:p + vl]
             p += vl
-        elif tag in (0, 7):  # kTypeDeletion / kTypeSingleDeletion
-            yield key, seq + i, 0, b""
-        else:
-            raise DocStoreError(f"unsupported WriteBatch record type {tag}")
+        if cf == 0:
+            yield key, seq + i, (1 if tag == _WB_PUT else 0), val
+        i += 1
 
 
 # --------------------------------------------------------------------------- safe pickle
@@ -282,7 +310,8 @@ class _Reduced:
 
 _MARK = object()
 _ALLOWED = {"numpy.core.multiarray._reconstruct", "numpy._core.multiarray._reconstruct", "numpy.ndarray",
-            "numpy.dtype", "numpy.core.multiarray.scalar", "numpy._core.multiarray.scalar"}
+            "numpy.dtype", "numpy.core.multiarray.scalar", "numpy._core.multiarray.scalar",
+            "numpy.core.numeric._frombuffer", "numpy._core.numeric._frombuffer"}  # (protocol-5 arrays)
 
 
 def _finish(o):
@@ -299,6 +328,14 @@ def _finish(o):
             if not isinstance(raw, (bytes, bytearray)):
                 raise DocStoreError("numpy scalar pickle with object payload")
             return np.frombuffer(bytes(raw), dtype=dt)[0]
+        if name and name.endswith("numeric._frombuffer"):  # protocol 5: (buffer, dtype, shape, order)
+            if len(o.args) != 4:
+                raise DocStoreError("malformed protocol-5 ndarray pickle")
+            raw, dt, shape, order = o.args[0], _finish(o.args[1]), o.args[2], o.args[3]
+            if not isinstance(raw, (bytes, bytearray)) or not isinstance(dt, np.dtype) or dt.hasobject:
+                raise DocStoreError("protocol-5 ndarray pickle with object payload")
+            a = np.frombuffer(bytes(raw), dtype=dt)
+            return a.reshape(tuple(shape), order="F" if order == "F" else "C").copy()
         if name and name.endswith("multiarray._reconstruct"):
             st = o.state
             if st is None or len(st) < 5:
@@ -427,10 +464,10 @@ def decode_rocksdict(b: bytes):
         return bytes(p)
     if t == 0x02:
         return p.decode("utf-8")
-    if t == 0x03:
-        return int.from_bytes(p, "little", signed=True)
-    if t == 0x04:
-        return struct.unpack("<d", p)[0]
+    if t in (0x03, 0x04):
+        # rocksdict's int / float payloads: their byte order is pinned by no reference artefact (the
+        # reference's folders use str keys and pickled values), so they are refused, not guessed
+        raise DocStoreError(f"rocksdict {'int' if t == 0x03 else 'float'} encoding is not supported (byte order unpinned)")
     if t == 0x05:
         return bool(p[0])
     if t == 0x06:
@@ -439,14 +476,24 @@ def decode_rocksdict(b: bytes):
 
 
 class RocksDictReader:
-    """The live entries of a rocksdict directory, read once: ``{key: value}`` (decoded)."""
+    """The live entries of a rocksdict directory, read once: ``{key: value}`` (decoded).
+
+    Every ``*.sst`` and ``*.log`` in the directory is read and each key resolves to its highest
+    sequence number.  Limitation: the live file set in MANIFEST is not consulted, so a table or log
+    that a crash left behind (or a flushed WAL still on disk) is read as well; that is exact for the
+    reference's persisted folders (one table, no stale files) but could revive a key whose tombstone a
+    bottommost compaction dropped.  A directory with several logs is reported with a warning."""
 
     def __init__(self, path: str):
         if not os.path.isdir(path):
             raise DocStoreError(f"{path} is not a directory")
         best = {}
         srcs = [read_sst(f) for f in sorted(glob.glob(os.path.join(path, "*.sst")))]
-        srcs += [read_wal(f) for f in sorted(glob.glob(os.path.join(path, "*.log")))]
+        logs = sorted(glob.glob(os.path.join(path, "*.log")))
+        if len(logs) > 1:
+            logger.warning("%s holds %d write-ahead logs; the reader does not consult MANIFEST's live set", path,
+                           len(logs))
+        srcs += [read_wal(f) for f in logs]
         for it in srcs:
             for key, seq, typ, val in it:
                 if typ not in (0, 1, 7):
