@@ -431,6 +431,22 @@ def pmc_traffic(tag, kernel):
         return None
 
 
+def rocprof_avg_ms(tag, kernel):
+    """Average duration (ms) of `kernel` in the newest committed rocprofv3 --kernel-trace --stats summary for
+    this workload tag (profiles/r*_<tag>_kernel_stats.csv), or None."""
+    import csv
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_kernel_stats.csv")))
+    if not files:
+        return None
+    try:
+        for row in csv.DictReader(open(files[-1])):
+            if kernel in row["Name"]:
+                return float(row["AverageNs"]) / 1e6, os.path.relpath(files[-1], HERE)
+    except Exception:
+        return None
+    return None
+
+
 def measured_mfma_peak():
     """Sustained FP4 MFMA rate measured by tools/probes/mfma_rate_probe (profiles/), or None."""
     try:
@@ -787,9 +803,14 @@ def main():
                     "frac": mb / (st["matrix"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                     "traffic": pmc_traffic(tag, "hamming_mfma_rows_kernel"),
                     "kernel": "hamming_mfma_rows_kernel (row-split FP4 MFMA scan, small batches)",
-                    "kernel_ms": st["matrix"], "algorithmic_bytes_per_launch": mb, "rows": rows_m,
+                    "kernel_ms": st["matrix"], "timing": "HIP events on the library's stream, this run",
+                    "algorithmic_bytes_per_launch": mb, "rows": rows_m,
                     "mfma": {"achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
                              "frac": ach / MFMA_FP4_PEAK_TOPS}}
+            rp = rocprof_avg_ms(tag, "hamming_mfma_rows_kernel")
+            if rp:  # the same kernel's rocprofv3 kernel-trace average (a profiled run of this workload)
+                roof["rocprof"] = {"avg_ms": rp[0], "achieved": mb / (rp[0] * 1e-3) / 1e9,
+                                   "frac": mb / (rp[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, "source": rp[1]}
     else:
         roof = dict(roof_scan_hbm, traffic=pmc_traffic(tag, "hamming_scan_kernel"),
                     kernel="hamming_scan_kernel (wavefront popcount)", kernel_ms=st["scan"])

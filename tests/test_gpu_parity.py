@@ -75,6 +75,27 @@ def test_encoders_random_batches_vs_oracle(dev, d):
             assert np.array_equal(r["minmax"].cpu().numpy(), mm), mode
 
 
+def test_encoders_persistent_loop_d1024(dev):
+    """d = 1024 runs the persistent encoder (each wave loops over vectors, the next one's 4 KiB in
+    flight): 9001 vectors = more than one vector per wave, an odd tail, flat rows (min == max), exact
+    ties with the mean, values beyond the global limit; bit-exact against the oracle in every mode."""
+    from vectorragquantization_amd.quant import encode
+    rng = np.random.default_rng(77)
+    n = 9001
+    X = (rng.standard_normal((n, 1024)) * rng.uniform(0.01, 2.0, (n, 1))).astype(np.float32)
+    X[17] = 0.25                                   # flat row: scale 0, mean == every element
+    X[4000, :512] = 1.0                            # half the elements exactly at the top
+    X[4000, 512:] = -1.0
+    X[8999] = np.round(X[8999] * 8) / 8            # many repeated values
+    for mode in ("int8g", "int16g", "int4g", "int8", "int4", "cohere"):
+        c, q, mm = O.encode_batch(mode, X, 0.3)
+        r = encode(mode, X, 0.3, dev)
+        assert np.array_equal(r["codes"].cpu().numpy(), c), mode
+        assert np.array_equal(r["q"].cpu().numpy(), q), mode
+        if mm is not None:
+            assert np.array_equal(r["minmax"].cpu().numpy(), mm), mode
+
+
 def test_int8_norms_exact(dev):
     from vectorragquantization_amd.quant import int8_row_norms
     rng = np.random.default_rng(1)

@@ -290,6 +290,165 @@ __global__ __launch_bounds__(EPB * 64) void encode_kernel(const void* __restrict
   }
 }
 
+// d = 1024 float modes (every BASELINE shape): persistent waves, each looping over vectors
+// v = gw, gw + nw, ...; the next vector's 4 KiB is loaded into registers while the current one is
+// encoded.  Lane l holds elements 256k + 4l + c (k, c < 4: four coalesced 1 KiB loads).
+//  * mean: the 4 KiB go to the wave's LDS slice once; lane 8g + j accumulates leaf g's column j
+//    (16 sequential adds, NumPy's order), then a 6-step butterfly (xor 1, 2, 4: the leaf's
+//    ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)); xor 8, 16, 32: the balanced tree over the 8 leaves) leaves
+//    the exact pairwise sum in every lane (each step adds the same two values in every lane pair);
+//  * min / max (local modes) and the quantised outputs come from the registers: q bytes / int16 /
+//    nibbles of elements 256k + 4l + c are stored per k as one coalesced 256 / 512 / 128 B row;
+//  * the code bytes from the LDS slice: lane l packs elements 16l..16l+15 (four conflict-free
+//    ds_read_b128) into bytes 2l, 2l+1 (one 128 B store per wave).
+constexpr int ENC_WPB = 4;                       // waves per workgroup (each on its own LDS slice)
+constexpr int ENC_SLICE = 1024 + 64;             // floats per wave slice (+ padding)
+
+template <int MODE>
+__device__ __forceinline__ void enc1024_load(float4 (&x)[4], const float* __restrict__ row, int l) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = *reinterpret_cast<const float4*>(row + 256 * k + 4 * l);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* __restrict__ xin, int64_t n,
+                                                                  double limit, uint8_t* __restrict__ codes,
+                                                                  void* __restrict__ qout, double* __restrict__ minmax) {
+  __shared__ __attribute__((aligned(16))) float smem[ENC_WPB * ENC_SLICE];
+  const int w = threadIdx.x >> 6, l = lane_id(), g = l >> 3, j = l & 7;
+  float* xs = smem + w * ENC_SLICE;
+  const int64_t nw = (int64_t)gridDim.x * ENC_WPB;
+  int64_t v = (int64_t)blockIdx.x * ENC_WPB + w;
+  if (v >= n) return;
+  float4 xn[4];
+  enc1024_load<MODE>(xn, xin + v * 1024, l);
+  float lim = 0.f, gscale = 0.f;
+  if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
+    lim = (float)limit;
+    gscale = (float)(127.0 / limit);
+  } else if constexpr (MODE == VRQ_ENC_INT16_GLOBAL) {
+    lim = (float)limit;
+    gscale = (float)(32767.0 / limit);
+  }
+  for (; v < n; v += nw) {
+    float4 xc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xc[k] = xn[k];
+    if (v + nw < n) enc1024_load<MODE>(xn, xin + (v + nw) * 1024, l);  // next vector in flight
+    float e[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      e[4 * k] = xc[k].x;
+      e[4 * k + 1] = xc[k].y;
+      e[4 * k + 2] = xc[k].z;
+      e[4 * k + 3] = xc[k].w;
+    }
+    // previous vector's LDS reads are complete before the slice is overwritten
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(xs + 256 * k + 4 * l) = xc[k];
+    wave_lds_sync();
+    float mean = 0.f;
+    if constexpr (MODE != VRQ_ENC_COHERE) {
+      const float* leaf = xs + 128 * g + j;
+      float r = leaf[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) r += leaf[8 * i];
+      r = r + __shfl_xor(r, 1, WAVE);
+      r = r + __shfl_xor(r, 2, WAVE);
+      r = r + __shfl_xor(r, 4, WAVE);
+      r = r + __shfl_xor(r, 8, WAVE);
+      r = r + __shfl_xor(r, 16, WAVE);
+      r = r + __shfl_xor(r, 32, WAVE);
+      mean = (float)((double)r / 1024.0);  // np.float32(sum) / np.intp(n) -> float32
+    }
+    // code bytes 2l, 2l+1 = elements 16l..16l+15 (MSB first)
+    {
+      const float4* p = reinterpret_cast<const float4*>(xs + 16 * l);
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 c = p[k];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int idx = 4 * k + q;  // element 16l + idx -> byte idx / 8, bit 7 - idx % 8
+          const bool bit = (MODE == VRQ_ENC_COHERE) ? (cv[q] > 0.f) : (cv[q] > mean);
+          bits |= (bit ? 1u : 0u) << ((idx < 8) ? 7 - idx : 23 - idx);
+        }
+      }
+      *reinterpret_cast<uint16_t*>(codes + v * 128 + 2 * l) = (uint16_t)bits;
+    }
+    float scale = gscale;
+    bool flat = false;
+    if constexpr (MODE == VRQ_ENC_INT4_GLOBAL || MODE == VRQ_ENC_INT8_LOCAL || MODE == VRQ_ENC_INT4_LOCAL) {
+      float mn = e[0], mx = e[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) {
+        mn = fminf(mn, e[i]);
+        mx = fmaxf(mx, e[i]);
+      }
+#pragma unroll
+      for (int m = 1; m < WAVE; m <<= 1) {
+        mn = fminf(mn, __shfl_xor(mn, m, WAVE));
+        mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
+      }
+      if constexpr (MODE != VRQ_ENC_INT4_GLOBAL) {
+        if (l == 0) {
+          minmax[2 * v] = (double)mn;
+          minmax[2 * v + 1] = (double)mx;
+        }
+      }
+      const float am = fmaxf(fabsf(mn), fabsf(mx));
+      flat = (mx == mn);
+      scale = flat ? 0.f : (float)((MODE == VRQ_ENC_INT8_LOCAL ? 127.0 : 7.0) / (double)am);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float* ek = e + 4 * k;
+      const int64_t o = v * 1024 + 256 * k + 4 * l;  // element index of ek[0]
+      if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float y = clampf(rintf(clampf(ek[c], -lim, lim) * scale), -127.f, 127.f);
+          wd |= ((uint32_t)(uint8_t)(int8_t)(int)y) << (8 * c);
+        }
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + o) = wd;
+      } else if constexpr (MODE == VRQ_ENC_INT16_GLOBAL) {
+        uint32_t wd[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float y = clampf(rintf(clampf(ek[c], -lim, lim) * scale), -32767.f, 32767.f);
+          wd[c >> 1] |= ((uint32_t)(uint16_t)(int16_t)(int)y) << (16 * (c & 1));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<int16_t*>(qout) + o) = make_uint2(wd[0], wd[1]);
+      } else if constexpr (MODE == VRQ_ENC_INT8_LOCAL) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int y = flat ? 0 : (int)(ek[c] * scale);  // astype(int8): truncation toward zero
+          wd |= ((uint32_t)(uint8_t)(int8_t)y) << (8 * c);
+        }
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + o) = wd;
+      } else {  // int4: nibble pairs, high = even index; bytes (o / 2), (o / 2) + 1
+        uint32_t hw = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c += 2) {
+          uint32_t byte4 = 0;
+          if (!flat) {
+            const int a = (int)clampf(rintf(ek[c] * scale), -8.f, 7.f) + 8;
+            const int b = (int)clampf(rintf(ek[c + 1] * scale), -8.f, 7.f) + 8;
+            byte4 = (uint32_t)(((a & 0x0f) << 4) | (b & 0x0f));
+          }
+          hw |= byte4 << (4 * c);
+        }
+        *reinterpret_cast<uint16_t*>(reinterpret_cast<int8_t*>(qout) + o / 2) = (uint16_t)hw;
+      }
+    }
+  }
+}
+
 // K7: ||x8 row||_2 in float64 from the exact integer sum of squares.
 __global__ __launch_bounds__(256) void int8_norms_kernel(const int8_t* __restrict__ x8, int64_t n, int dim,
                                                          double* __restrict__ out) {
@@ -362,6 +521,34 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
   const int64_t qrow = mode == VRQ_ENC_INT16_GLOBAL                              ? 2 * (int64_t)dim
                        : (mode == VRQ_ENC_INT4_GLOBAL || mode == VRQ_ENC_INT4_LOCAL) ? (int64_t)(dim + 1) / 2
                                                                                     : (int64_t)dim;
+  if (dim == 1024 && mode != VRQ_ENC_BIN_INT16) {
+    // persistent waves: 16 per CU (4 workgroups of 4 waves), each looping over vectors
+    const int64_t wgs = (n + ENC_WPB - 1) / ENC_WPB;
+    const dim3 grid((unsigned)(wgs < 256 * 4 ? wgs : 256 * 4)), block(ENC_WPB * 64);
+    const float* xf = (const float*)x;
+    switch (mode) {
+      case VRQ_ENC_INT8_GLOBAL:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+      case VRQ_ENC_INT16_GLOBAL:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+      case VRQ_ENC_INT4_GLOBAL:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+      case VRQ_ENC_INT8_LOCAL:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+      case VRQ_ENC_INT4_LOCAL:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+      default:
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_COHERE>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        break;
+    }
+    VRQ_LAUNCH_CHECK();
+    return VRQ_OK;
+  }
   constexpr int64_t kMaxLaunch = 1 << 24;
   for (int64_t v0 = 0; v0 < n; v0 += kMaxLaunch) {
     const int64_t nv = n - v0 < kMaxLaunch ? n - v0 : kMaxLaunch;

@@ -71,6 +71,11 @@
 #ifndef VRQ_G5_DMA_PROBE
 #define VRQ_G5_DMA_PROBE 0
 #endif
+// Phase-III thresholded pass: stage the int8 tiles through registers (global_load_dwordx4 during
+// tile t-1, ds_write_b128 into the image during tile t, for tile t+1) instead of LDS-DMA
+#ifndef VRQ_G5_REGSTAGE
+#define VRQ_G5_REGSTAGE 0
+#endif
 
 namespace vrq {
 namespace g5 {
@@ -250,11 +255,14 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
   // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
   // packed tile t+1 expanded into the unpacked ring (2 tiles) during tile t.
-  constexpr int NP = P3 ? VRQ_G5_NP3 : 4;
+  // RS (register staging, Phase-III thresholded pass): ring of 2 images; during tile t each wave
+  // writes its 8 staged rows of tile t+1 into the free image and loads its rows of tile t+2
+  constexpr bool RS = P3 && !DENSE && VRQ_G5_REGSTAGE;
+  constexpr int NP = RS ? 2 : P3 ? VRQ_G5_NP3 : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
   constexpr int PPW = P3 ? 9 : 1;                     // vector-memory instructions per wave per tile
-  constexpr bool NREG = P3 && VRQ_G5_NORM_REG;        // (8 LDS-DMA rows + 1 norm load, or 9 LDS-DMA)
+  constexpr bool NREG = P3 && (VRQ_G5_NORM_REG || RS);  // (8 LDS-DMA rows + 1 norm load, or 9 LDS-DMA)
   constexpr int AHEAD = NP - 1;                       // tiles the DMA runs ahead
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   __shared__ int32_t lcnt[GW * GQW];  // per-(query, this chunk) list lengths, one row of 32 per wave
@@ -375,6 +383,20 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         issue_tiny(i);
       else
         issue_piece(dma_tile(t, t), i);
+    }
+  }
+  // RS: this wave's 8 rows of the staged tile (tile t+1 during tile t), one 16-B chunk per lane in
+  // the image's order (row 8w+i, chunk l ^ (row & 15): the same image the LDS-DMA fills)
+  v4i stg[RS ? 8 : 1];
+  auto stage_load = [&](int tt, int i) {
+    const uint8_t* base = src + (row0 + tstart(tt) + 8 * w) * RB;
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(stg[RS ? i : 0]) : "v"(loff[P3 ? i : 0]), "s"(base) : "memory");
+  };
+  if constexpr (RS) {
+    if (ntiles > 1) {  // (ntiles > 1: no tiny chunk)
+      issue_norm(1, nvr[1]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stage_load(1, i);
     }
   }
 
@@ -498,8 +520,18 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
     // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
     // the slots the DMA of this tile overwrites.
-    {  // the DMA of the tile needed now (t; Phase II: t+1) landed; the INF tiles issued after it may
-       // stay in flight (in the chunk's last tiles: wait for everything)
+    if constexpr (RS) {
+      // tile 0: its DMA and norm landed (tile 1's norm + 8 staged rows may stay in flight); later
+      // tiles were written by this wave's ds_writes during the previous tile
+      if (t == 0) {
+        if (ntiles > 1)
+          wait_vm<9>();
+        else
+          wait_vm<0>();
+      }
+      wait_lgkm0();
+    } else {  // the DMA of the tile needed now (t; Phase II: t+1) landed; the INF tiles issued after it may
+              // stay in flight (in the chunk's last tiles: wait for everything)
       constexpr int NEED = P3 ? 0 : 1, INF = AHEAD - 1 - NEED;
       if (t + NEED + INF < ntiles)
         wait_vm<INF * PPW>();
@@ -560,7 +592,26 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       }
       asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
       // DMA of tile t + AHEAD, spread over the MFMA shadow
-      if constexpr (P3) {
+      if constexpr (RS) {
+        // piece i at k-step 2 + DS*i: write staged row i of tile t+1 (loaded during tile t-1; the 8
+        // operations issued after it -- rows i+1..7 of tile t+1, tile t+2's norm and rows 0..i-1 --
+        // may stay in flight), then load row i of tile t+2 into the same registers
+        constexpr int DS = VRQ_G5_DMA_STRIDE;
+        if constexpr (s >= 2 && s < 2 + DS * 8 && (s - 2) % DS == 0) {
+          constexpr int i = (s - 2) / DS;
+          const bool wr = t + 1 < ntiles, ld = t + 2 < ntiles;
+          if constexpr (i == 0)
+            if (ld) issue_norm(t + 2, nvr[p]);  // (nv holds this tile's norm already)
+          if (wr) {
+            if (ld)
+              asm volatile("s_waitcnt vmcnt(8)" : "+v"(stg[i])::"memory");
+            else
+              asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[i])::"memory");
+            lds_write128(sm0 + (uint32_t)(sl1 * PKT + (8 * w + i) * 1024 + l * 16), stg[i]);
+          }
+          if (ld) stage_load(t + 2, i);
+        }
+      } else if constexpr (P3) {
         constexpr int DS = VRQ_G5_DMA_STRIDE, NPC3 = NREG ? 8 : 9;
         if constexpr (s >= 2 && s < 2 + DS * NPC3 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2)) {
           if constexpr (NREG && s == 2)
@@ -1006,7 +1057,8 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   // chunks keep the query blocks that share a chunk closer in time, so they share its L2 lines
   const int cm = tuning_int("VRQ_GEMM_CHUNK_MULT", kChunkMult);
   const int mult = cm >= 1 ? cm : kChunkMult;
-  const int want = (256 / p->nqb > 0 ? 256 / p->nqb : 1) * mult;
+  const int want1 = 256 / p->nqb > 0 ? 256 / p->nqb : 1;  // one workgroup per CU and query block
+  const int want = want1 * mult;
   // sample rows: the sampled threshold alone admits ~k * n / S rows per query; aim at FIN_CAP /
   // CAP_MULT so that the margin's extra rows still fit (VRQ_GEMM_SAMPLE_DIV overrides n / S)
   int64_t S = (int64_t)((double)CAP_MULT * (double)k * (double)n / (double)FIN_CAP);
@@ -1017,7 +1069,7 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   if (S > n) S = n;
   // sample chunks: one per CU and query block, and >= 2k / 32 so the select sees >= 2k lane maxima
   // per query (fewer than k would leave thr = -inf: every row a candidate)
-  int64_t nsc = want > (2 * (int64_t)k + GRT - 1) / GRT ? want : (2 * (int64_t)k + GRT - 1) / GRT;
+  int64_t nsc = want1 > (2 * (int64_t)k + GRT - 1) / GRT ? want1 : (2 * (int64_t)k + GRT - 1) / GRT;
   int64_t scr = ((S + nsc - 1) / nsc + GRT - 1) / GRT * GRT;
   nsc = (S + scr - 1) / scr;
   p->scr = scr;

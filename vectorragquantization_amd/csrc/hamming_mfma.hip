@@ -40,6 +40,12 @@
 #ifndef VRQ_BISECT
 #define VRQ_BISECT 0
 #endif
+// hit extraction of a flagged (M-block, n-block): 1 = per-lane 16-bit hit masks and one staged
+// entry per lane when no lane holds two hits (the usual case), the 16-ballot walk otherwise;
+// 0 = always the 16-ballot walk
+#ifndef VRQ_HIT_FAST
+#define VRQ_HIT_FAST 1
+#endif
 
 namespace vrq {
 
@@ -446,6 +452,40 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       }
     }
   };
+  // Branch-light form: per lane a 16-bit mask of its registers above the threshold; when no lane
+  // holds two hits (one ballot proves it) each hit lane stages one entry -- its single hit is its
+  // largest register (the others are <= hp), found by a max3 tree, its query row by the mask's
+  // lowest bit -- at its rank among the hit lanes.  Otherwise the 16-ballot walk above.
+  auto block_hits_fast = [&](const v16f& a, int m, int pc, float hp, int rel7) __attribute__((always_inline)) {
+    if constexpr (!VRQ_HIT_FAST) {
+      block_hits(a, m, pc, hp, rel7);
+    } else {
+      uint32_t m16 = 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) m16 |= (a[g] > hp ? 1u : 0u) << g;
+      if (__ballot((m16 & (m16 - 1)) != 0)) {  // some lane holds two or more hits (rare)
+        block_hits(a, m, pc, hp, rel7);
+      } else {
+        const uint64_t lanes = __ballot(m16 != 0);
+        if (m16) {
+          const v16i b = __builtin_bit_cast(v16i, a);  // >= 0 patterns order like their floats
+          const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
+          const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
+          const float mx = __int_as_float(max(max(max(x0, x1), x2), max(max(x3, x4), b[15])));
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0));
+          int lo = l;
+          asm volatile("" : "+v"(lo));
+          const int g = __builtin_ctz(m16);
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+          const int v = pc - (int)(2.0f * mx);
+          const int pos = nst + below < STG ? nst + below : STG;
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
+        }
+        nst += __popcll(lanes);
+      }
+    }
+  };
   auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
   // DENSE: the 16 values v = dist - pc(q) of block (m, n-block) (row lr of the chunk) fold into this
   // lane's running minima; only those leave the kernel (dense_out)
@@ -624,7 +664,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
               const float hp = 0.5f * (float)pc;
               static_for<0, MB>([&](auto M) {
                 constexpr int mm = decltype(M)::value;
-                if (hitm[mm]) block_hits(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
+                if (hitm[mm]) block_hits_fast(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
               });
             }
           }
@@ -674,7 +714,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       if constexpr (DENSE)
         block_dense(acc[1][m], m, pcvP, lr);
       else
-        if (any_above(acc[1][m], hp)) block_hits(acc[1][m], m, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
+        if (any_above(acc[1][m], hp)) block_hits_fast(acc[1][m], m, pc, hp, 96 + ri);  // rel7 against tile ntiles-2
     });
     if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }

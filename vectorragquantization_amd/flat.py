@@ -62,7 +62,8 @@ def flat_ip_topk(xf: torch.Tensor, x8: torch.Tensor, inv_scale: torch.Tensor, bo
     N.check(lib.vrq_flat_ip_topk(N.ptr(xf), N.ptr(x8), N.ptr(inv_scale), N.ptr(bounds), n, qf.shape[1], row_offset,
                                  N.ptr(qf), nq, k, flags, N.ptr(cnt), N.ptr(rows), N.ptr(scores),
                                  N.ptr(workspace), workspace.numel(), N.stream_handle(dev)), "vrq_flat_ip_topk")
-    if bool((cnt < 0).any()):
+    stages = flags & (N.VRQ_GEMM_STAGE_SAMPLE | N.VRQ_GEMM_STAGE_MAIN | N.VRQ_GEMM_STAGE_FINISH)
+    if (not stages or stages & N.VRQ_GEMM_STAGE_FINISH) and bool((cnt < 0).any()):
         # only with VRQ_GEMM_NO_FALLBACK in flags: the library left queries it could not serve on the
         # matrix path unwritten (count -1) instead of running the exact scan
         raise N.VrqNativeError("vrq_flat_ip_topk: queries needed the exact fallback, which VRQ_GEMM_NO_FALLBACK disabled")
