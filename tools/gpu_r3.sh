@@ -17,6 +17,10 @@ if [ -n "${G5LIBS:-}" ]; then
   VRQ_LIBS=$G5LIBS timeout -k 10 400 python -u tools/gemm_probe.py ${G5ARGS:---n 10000000 --stages 16,32} > $OUT/g5_probe.jsonl 2> $OUT/g5_probe.err || { echo G5_FAIL; tail -20 $OUT/g5_probe.err; exit 1; }
   cat $OUT/g5_probe.jsonl
 fi
+if [ -n "${ENCLIBS:-}" ]; then
+  VRQ_LIBS=$ENCLIBS timeout -k 10 300 python -u tools/enc_probe.py > $OUT/enc_probe.jsonl 2> $OUT/enc_probe.err || { echo ENC_FAIL; tail -20 $OUT/enc_probe.err; exit 1; }
+  cat $OUT/enc_probe.jsonl
+fi
 for c in ${BENCHES:-}; do
   timeout -k 10 ${BENCH_T:-600} python -u bench.py --config $c ${BENCH_EXTRA:-} > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { echo BENCH_FAIL $c; tail -30 $OUT/bench_$c.err; exit 1; }
   python -c "

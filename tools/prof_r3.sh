@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-3 profiling pass (run on the GPU box via gpurun): for each "config:nq" in RUNS, a rocprofv3
+# kernel-trace --stats run of a short bench line, then (PMC=1) separate FETCH_SIZE and WRITE_SIZE
+# passes (one counter block per pass, MI355X_MICROARCH.md), condensed by tools/summarize_profile.py
+# into gpurun_out/$TAG/<config>_nq<nq>/summary.json.  Each GPU step is time-limited; the chain stops
+# at the first failure.
+#   RUNS="c3:1 c3:8 c3:64 c2:1024 c4:1024 c5:1024"  TAG=name  PMC=1|0  BARGS="extra bench args"
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for run in ${RUNS:-c3:8}; do
+  CFG=${run%%:*}; NQ=${run#*:}
+  OUT=gpurun_out/${TAG:-prof_r3}/${CFG}_nq${NQ}
+  mkdir -p $OUT
+  B="--config $CFG --nq $NQ --no-cpu-baseline --no-recall --no-encode ${BARGS:-}"
+  timeout -k 10 ${PT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 5 --warmup 1 $B > $OUT/bench_trace.json 2> $OUT/bench_trace.err || { echo TRACE_FAIL $run; tail -20 $OUT/bench_trace.err; exit 1; }
+  if [ "${PMC:-1}" = "1" ]; then
+    timeout -k 10 ${PT:-400} rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 $B > $OUT/pmc_fetch.log 2>&1 || { echo FETCH_FAIL $run; tail -20 $OUT/pmc_fetch.log; exit 1; }
+    timeout -k 10 ${PT:-400} rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 $B > $OUT/pmc_write.log 2>&1 || { echo WRITE_FAIL $run; tail -20 $OUT/pmc_write.log; exit 1; }
+  fi
+  python3 tools/summarize_profile.py $OUT $OUT/summary.json ${CFG}_nq${NQ} > /dev/null
+  python3 - <<PY
+import json
+d = json.load(open("$OUT/summary.json"))
+print("== $run", json.load(open("$OUT/bench_trace.json"))["phase_ms"])
+for r in d.get("kernel_stats", []):
+    if float(r["Percentage"]) > 0.5:
+        print(f'  {r["Name"].split("(")[0][:70]:70s} calls {r["Calls"]:>5s} avg_us {float(r["AverageNs"])/1e3:10.2f}')
+print("  MB/launch", {k: round(v / 1e6, 1) for k, v in d.get("bytes_per_launch", {}).items()})
+PY
+done
+echo done

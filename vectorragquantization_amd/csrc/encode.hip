@@ -302,6 +302,10 @@ __global__ __launch_bounds__(EPB * 64) void encode_kernel(const void* __restrict
 //  * the code bytes from the LDS slice: lane l packs elements 16l..16l+15 (four conflict-free
 //    ds_read_b128) into bytes 2l, 2l+1 (one 128 B store per wave).
 constexpr int ENC_WPB = 4;                       // waves per workgroup (each on its own LDS slice)
+#ifndef VRQ_ENC_WGS_PER_CU
+#define VRQ_ENC_WGS_PER_CU 0                     // persistent workgroups per CU (0: one vector per wave)
+#endif
+constexpr bool kEncPersist = VRQ_ENC_WGS_PER_CU > 0;
 constexpr int ENC_SLICE = 1024 + 64;             // floats per wave slice (+ padding)
 
 template <int MODE>
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
     float4 xc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) xc[k] = xn[k];
-    if (v + nw < n) enc1024_load<MODE>(xn, xin + (v + nw) * 1024, l);  // next vector in flight
+    if (kEncPersist && v + nw < n) enc1024_load<MODE>(xn, xin + (v + nw) * 1024, l);  // next vector in flight
     float e[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -522,31 +526,43 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
                        : (mode == VRQ_ENC_INT4_GLOBAL || mode == VRQ_ENC_INT4_LOCAL) ? (int64_t)(dim + 1) / 2
                                                                                     : (int64_t)dim;
   if (dim == 1024 && mode != VRQ_ENC_BIN_INT16) {
-    // persistent waves: 16 per CU (4 workgroups of 4 waves), each looping over vectors
+    // one vector per wave (the measured best: 0.63-0.71 of HBM vs 0.58-0.61 for 4-6 persistent
+    // workgroups per CU, tools/enc_probe.py), launches of at most 2^22 workgroups (2^24 vectors, a
+    // dispatch below 2^32 work-items); or VRQ_ENC_WGS_PER_CU persistent workgroups per CU, each
+    // wave looping over vectors
     const int64_t wgs = (n + ENC_WPB - 1) / ENC_WPB;
-    const dim3 grid((unsigned)(wgs < 256 * 4 ? wgs : 256 * 4)), block(ENC_WPB * 64);
-    const float* xf = (const float*)x;
+    constexpr int64_t kPersist = 256 * VRQ_ENC_WGS_PER_CU, kMaxWgs = int64_t(1) << 22;
+    const int64_t lw = kEncPersist ? wgs : (wgs > kMaxWgs ? kMaxWgs : wgs);  // workgroups' vectors per launch
+    for (int64_t w0 = 0; w0 < wgs; w0 += lw) {
+    const int64_t v0 = w0 * ENC_WPB, nv = n - v0 < lw * ENC_WPB ? n - v0 : lw * ENC_WPB;
+    const int64_t g = (nv + ENC_WPB - 1) / ENC_WPB;
+    const dim3 grid((unsigned)(kEncPersist && g > kPersist ? kPersist : g)), block(ENC_WPB * 64);
+    const float* xf = (const float*)x + v0 * 1024;
+    uint8_t* cv = codes + v0 * 128;
+    void* qv = (uint8_t*)q + v0 * qrow;
+    double* mv = minmax ? minmax + 2 * v0 : nullptr;
     switch (mode) {
       case VRQ_ENC_INT8_GLOBAL:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_GLOBAL>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
       case VRQ_ENC_INT16_GLOBAL:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT16_GLOBAL>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
       case VRQ_ENC_INT4_GLOBAL:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_GLOBAL>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
       case VRQ_ENC_INT8_LOCAL:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT8_LOCAL>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
       case VRQ_ENC_INT4_LOCAL:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_INT4_LOCAL>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
       default:
-        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_COHERE>, grid, block, 0, s, xf, n, limit, codes, q, minmax);
+        hipLaunchKernelGGL(encode1024_kernel<VRQ_ENC_COHERE>, grid, block, 0, s, xf, nv, limit, cv, qv, mv);
         break;
     }
     VRQ_LAUNCH_CHECK();
+    }
     return VRQ_OK;
   }
   constexpr int64_t kMaxLaunch = 1 << 24;

@@ -42,8 +42,8 @@
 #include "vrq_internal.h"
 
 // tools/build_g5_variants.sh compiles this file with VRQ_G5_BISECT bits set to time the matrix pass
-// with parts removed (1: threshold test, 2: LDS-DMA, 4: tile barrier, 8: MFMA; 2/4/8 give wrong
-// results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
+// with parts removed (1: threshold test, 2: LDS-DMA, 4: tile barrier, 8: MFMA, 16: candidate
+// flush; 2/4/8/16 give wrong results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
 // the library build.
 #ifndef VRQ_G5_BISECT
 #define VRQ_G5_BISECT 0
@@ -63,8 +63,24 @@
 #ifndef VRQ_G5_NORM_REG
 #define VRQ_G5_NORM_REG 0  // Phase III: the tile's norms by a plain global load into registers (1) instead of LDS-DMA
 #endif
-#ifndef VRQ_G5_UREC
-#define VRQ_G5_UREC 1  // thresholded pass: flush recomputes u from the still-live accumulators (no ures[] file)
+#ifndef VRQ_G5_STAGE
+// thresholded pass: 1 = a tile's hits (at most one per lane: the usual case) go to a per-wave LDS
+// stage by wave-prefix positions (no atomic, no wait), drained into the per-(query, chunk) lists
+// once per chunk; 0 = every hit straight to its list (LDS atomic + wait + global store per hit)
+#define VRQ_G5_STAGE 1
+#endif
+constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave << 26 | chunk row)
+#ifndef VRQ_G5_SEED
+// Phase-II thresholded pass: the accumulators start at -ceil(thr) (an integer seed per query: the
+// binary u is the integer dot), so a test is one integer max per accumulator register and the flush
+// re-derives the hit bits (acc >= 0) from the still-live accumulators
+#define VRQ_G5_SEED 1
+#endif
+#ifndef VRQ_G5_HIT
+// thresholded pass, per-lane record of the tests of a tile: 2 = a hit bitmask built by the tests (the
+// flush reads it: no recomputation); 1 = the running max only, the flush recomputes u - thr from the
+// still-live accumulators; 0 = a ures[] register file of the tests' values
+#define VRQ_G5_HIT 2
 #endif
 // timing-only probes of the DMA's cost (wrong results): 1 = every tile's DMA reads the chunk's first
 // tile (L2-resident source), 2 = the pieces are plain global loads into a discarded register (no LDS write)
@@ -91,6 +107,23 @@ constexpr int NMB = 3 - NPC;         // 32-query M-blocks per wave
 constexpr int GQW = 32 * NMB;        // queries per wave
 constexpr int GQB = GW * GQW;        // queries per workgroup
 constexpr int NE = 16 * NMB;         // threshold tests per lane per tile
+#ifndef VRQ_G5_W8
+// Phase-III passes: 8 waves (two per SIMD) of 32 queries instead of 4 of 64; a SIMD's second wave
+// keeps its matrix core busy while the first issues its threshold tests and LDS-DMA pieces
+// (10M x 1024, nq = 1024: main pass 8.8 vs 9.5 ms, tools/probes)
+#define VRQ_G5_W8 1
+#endif
+#ifndef VRQ_G5_NP3_W8
+#define VRQ_G5_NP3_W8 2  // the 8-wave layout's DMA ring (tile t+1 streamed during tile t)
+#endif
+// wave layout of a matrix pass: W waves of MB 32-query M-blocks (W * 32 * MB = GQB queries per
+// workgroup either way), RPW rows of each 32-row tile streamed per wave
+template <int PH>
+struct KShape {
+  static constexpr bool W8 = PH != VRQ_GEMM_BINARY && VRQ_G5_W8 && NPC == 1;
+  static constexpr int W = W8 ? 8 : GW, MB = W8 ? 1 : NMB, QW = 32 * MB, NE = 16 * MB, RPW = 32 / W;
+  static_assert(W * QW == GQB, "query block");
+};
 // planning target for the candidates per query (the sample size follows from it), and the
 // per-(query, chunk) list capacity as a multiple of the hits the sample predicts (one piece: ~4x
 // wider margin)
@@ -246,26 +279,32 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
 // RETRY: the retry pass of launch_finish (same code; a separate symbol so kernel traces and counter
 // summaries keep the main pass's per-launch figures apart from the retry's near-empty launch).
 template <int PH, bool DENSE, bool RETRY = false>
-__global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
+__global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     const uint8_t* __restrict__ src, const double* __restrict__ norms, int64_t n, const int8_t* __restrict__ qa,
     int nq, const float* __restrict__ thr, uint32_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int nchunks, int nqb, float* __restrict__ dv, int64_t dv_stride,
     const int32_t* __restrict__ qbflag) {
   constexpr bool P3 = PH == VRQ_GEMM_INT8_COSINE;
+  constexpr int KW = KShape<PH>::W, KMB = KShape<PH>::MB, KQW = KShape<PH>::QW, KNE = KShape<PH>::NE;
+  constexpr int RPW = KShape<PH>::RPW;               // Phase III: tile rows streamed per wave
+  constexpr int NA = NPC == 2 ? 2 : KMB;             // A fragment sets per wave (pieces or M-blocks)
   // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
   // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
   // packed tile t+1 expanded into the unpacked ring (2 tiles) during tile t.
   // RS (register staging, Phase-III thresholded pass): ring of 2 images; during tile t each wave
   // writes its 8 staged rows of tile t+1 into the free image and loads its rows of tile t+2
   constexpr bool RS = P3 && !DENSE && VRQ_G5_REGSTAGE;
-  constexpr int NP = RS ? 2 : P3 ? VRQ_G5_NP3 : 4;
+  constexpr int NP = RS ? 2 : P3 ? (KShape<PH>::W8 ? VRQ_G5_NP3_W8 : VRQ_G5_NP3) : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
-  constexpr int PPW = P3 ? 9 : 1;                     // vector-memory instructions per wave per tile
+  constexpr int PPW = P3 ? RPW + 1 : 1;               // vector-memory instructions per wave per tile
   constexpr bool NREG = P3 && (VRQ_G5_NORM_REG || RS);  // (8 LDS-DMA rows + 1 norm load, or 9 LDS-DMA)
   constexpr int AHEAD = NP - 1;                       // tiles the DMA runs ahead
+  static_assert(!(RS && KShape<PH>::W8), "register staging assumes 4 waves");
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
-  __shared__ int32_t lcnt[GW * GQW];  // per-(query, this chunk) list lengths, one row of 32 per wave
+  constexpr bool STAGE = !DENSE && VRQ_G5_STAGE;
+  // per-(query, this chunk) list lengths (one row per wave), then each wave's hit stage
+  __shared__ int32_t lcnt[KW * KQW + (STAGE ? KW * STG5 : 0)];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l = lane_id(), r = l & 31, h = l >> 5;
   const int L = xcd_logical(blockIdx.x, gridDim.x);
@@ -297,7 +336,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   uint32_t loff[P3 ? 8 : 1];
   if constexpr (P3) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) loff[i] = (uint32_t)(i * 1024 + ((l ^ ((8 * w + i) & 15)) << 4));
+    for (int i = 0; i < RPW; ++i) loff[i] = (uint32_t)(i * 1024 + ((l ^ ((RPW * w + i) & 15)) << 4));
   } else {
     const int rr = 8 * w + (l >> 3);
     loff[0] = (uint32_t)((l >> 3) * 128 + (((l & 7) ^ ((rr >> 1) & 7)) << 4));
@@ -311,7 +350,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   auto dma_tile = [&](int t, int slot_i) {  // whole tiles (not tiny)
     const int64_t tr0 = row0 + (VRQ_G5_DMA_PROBE == 1 ? 0 : tstart(t));
     DmaTile d;
-    d.gsrc = src + (tr0 + 8 * w) * RB;
+    d.gsrc = src + (tr0 + (P3 ? RPW : 8) * w) * RB;
     d.gnrm = reinterpret_cast<const uint8_t*>(norms + tr0);
     d.lds = smem + slot_i * PKT;
     return d;
@@ -319,13 +358,13 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   auto issue_piece = [&](const DmaTile& d, int i) {
     // (pointer arguments through locals: a compound expression here makes the host-side compile
     // silently drop the kernel's launch stub)
-    if (P3 && i == 8) {
+    if (P3 && i == RPW) {
       const uint8_t* g = d.gnrm + 4 * l;
       __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(d.lds + T3), 4, 0, 0);
       return;
     }
     const uint8_t* g = d.gsrc + loff[P3 ? i : 0];
-    uint8_t* ld = d.lds + (P3 ? (8 * w + i) * 1024 : w * 1024);
+    uint8_t* ld = d.lds + (P3 ? (RPW * w + i) * 1024 : w * 1024);
     if constexpr (VRQ_G5_DMA_PROBE == 2) {
       v4i sink;
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sink) : "v"(g) : "memory");
@@ -335,18 +374,18 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     }
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
-    if (P3 && i == 8) {
+    if (P3 && i == RPW) {
       int64_t nr = row0 + (l >> 1);
       nr = nr < row1 ? nr : row1 - 1;
       const uint8_t* g = reinterpret_cast<const uint8_t*>(norms + nr) + 4 * (l & 1);
       __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + T3), 4, 0, 0);
       return;
     }
-    const int rr = P3 ? 8 * w + i : 8 * w + (l >> 3);
+    const int rr = P3 ? RPW * w + i : 8 * w + (l >> 3);
     int64_t row = row0 + rr;
     row = row < row1 ? row : row1 - 1;
     const uint8_t* g = src + row * RB + (P3 ? ((l ^ (rr & 15)) << 4) : ((((l & 7) ^ ((rr >> 1) & 7))) << 4));
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + (P3 ? (8 * w + i) * 1024 : w * 1024)),
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + (P3 ? (RPW * w + i) * 1024 : w * 1024)),
                                      16, 0, 0);
   };
   // Phase II expansion: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r, c = 2w + h
@@ -378,7 +417,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
       else issue_norm(1, nvr[1]);
     }
 #pragma unroll
-    for (int i = 0; i < (NREG ? 8 : PPW); ++i) {
+    for (int i = 0; i < (NREG ? RPW : PPW); ++i) {
       if (tiny)
         issue_tiny(i);
       else
@@ -401,11 +440,11 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   }
 
   // A fragments of this wave's 32 queries, both pieces, all 32 k-steps -> accumulator file
-  const int qbase = qb * GQB + w * GQW;
-  v4i A[2][GKS];  // [piece] (two pieces) or [M-block] (one piece)
+  const int qbase = qb * GQB + w * KQW;
+  v4i A[2][GKS];  // [piece] (two pieces) or [M-block] (one piece); NA of them used
   {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NA; ++j) {
       const int8_t* qp = NPC == 2 ? qa + (int64_t)(qbase + r) * QA_BYTES + j * 1024 + h * 16
                                   : qa + (int64_t)(qbase + 32 * j + r) * QA_BYTES + h * 16;
 #pragma unroll
@@ -413,14 +452,24 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     }
   }
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+  for (int p = 0; p < NA; ++p)
 #pragma unroll
     for (int s = 0; s < GKS; ++s) asm volatile("" : "+a"(A[p][s]));
   // test e of a lane: M-block e >> 4, accumulator register g = e & 15 -> query row of the wave
   auto qrow = [&](int e) { return 32 * (e >> 4) + ((e & 3) + 8 * ((e >> 2) & 3) + 4 * h); };
-  float th[NE];
+  float th[KNE];
 #pragma unroll
-  for (int e = 0; e < NE; ++e) th[e] = DENSE ? 0.f : thr[qbase + qrow(e)];
+  for (int e = 0; e < KNE; ++e) th[e] = DENSE ? 0.f : thr[qbase + qrow(e)];
+  constexpr bool SEED2 = !P3 && !DENSE && NPC == 1 && VRQ_G5_SEED;
+  v16i seed[SEED2 ? 2 : 1];  // SEED2: -ceil(thr) of each accumulator register's query, clamped
+  if constexpr (SEED2) {
+#pragma unroll
+    for (int e = 0; e < KNE; ++e) {
+      const float c = ceilf(th[e]);  // +-inf / huge thresholds: always / never a hit
+      seed[e >> 4][e & 15] = c <= -1073741824.f ? 1073741824 : c >= 1073741824.f ? -1073741824 : -(int)c;
+    }
+  }
+  int imax = INT32_MIN, iodd = 0;  // SEED2: running max of the seeded accumulators of the tested tile
 
   // Phase III: B fragment of k-step s for lane (r, h) = 16-B chunk 2s+h of tile row r, at slot
   // r*64 + ((2s+h) ^ (r & 15)) = r*64 + 16*(s>>3) + off[s&7]
@@ -428,19 +477,23 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) boff[j] = (uint32_t)(((((2 * j) ^ (r & 14)) | (h ^ (r & 1))) << 4) + r * 1024);
 
-  const uint32_t lc0 = lds_addr(lcnt + w * GQW);
-  if (!DENSE && l < GQW) lcnt[w * GQW + l] = 0;  // made visible by the first tile's barrier
-  v16i acc[2][2];        // [tile parity][piece]
+  const uint32_t lc0 = lds_addr(lcnt + w * KQW);
+  const uint32_t sg0 = lds_addr(lcnt + KW * KQW + (STAGE ? w * STG5 : 0));  // this wave's hit stage
+  int nst = 0;  // staged entries (wave-uniform)
+  if (!DENSE && l < KQW) lcnt[w * KQW + l] = 0;  // made visible by the first tile's barrier
+  v16i acc[2][2] = {};   // [tile parity][piece or M-block]
   // results of the previous tile (flushed at the top of the next-but-one tile): the sample pass
   // keeps u; the thresholded pass keeps u - thr (a hit iff >= 0; NaN never) and their running max.
-  // UREC: the thresholded pass keeps only the running max; the rare flush of a wave with a hit
-  // recomputes u - thr from the tile's accumulators, which stay live until the next-but-one tile's
-  // first MFMA (32 VGPRs fewer than a ures[] file)
-  constexpr bool UREC = !DENSE && VRQ_G5_UREC;
-  float ures[UREC ? 1 : NE];
+  // UREC: the thresholded pass keeps only the running max; a flush recomputes u - thr from the
+  // tile's accumulators, which stay live until the next-but-one tile's first MFMA.  HMASK: each test
+  // shifts its hit bit into hm (test e -> bit KNE-1-e), the flush reads hm.  Both: no ures[] file.
+  constexpr bool HMASK = !DENSE && VRQ_G5_HIT == 2;
+  constexpr bool UREC = !DENSE && VRQ_G5_HIT >= 1;
+  float ures[UREC ? 1 : KNE];
   float umax = -__builtin_inff(), uodd = 0.f;
+  uint32_t hm = 0;
 #pragma unroll
-  for (int e = 0; e < (UREC ? 1 : NE); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
+  for (int e = 0; e < (UREC ? 1 : KNE); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
   float invc = 0.f, invp = 0.f, invpp = 0.f;  // Phase III 1/||x|| of tiles t, t-1, t-2 (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
@@ -455,34 +508,80 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     else
       return P3 ? fmaf(u, inv, -th[e]) : u - th[e];
   };
+  // hit of query-in-wave ql at chunk row cr -> its (query, chunk) list (position from this wave's LDS
+  // counter; a list past capc keeps counting, which the finish kernel reads as an overflow)
+  auto to_list = [&](int ql, int cr) {
+    int pos;
+    lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+    if (pos < capc) cand[(int64_t)(qbase + ql) * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + cr);
+  };
+  // the staged entries -> lists (once per chunk, or when the stage is nearly full)
+  auto drain = [&]() {
+    for (int i0 = 0; i0 < nst; i0 += 64) {
+      const int i = i0 + l;
+      int e = 0;
+      if (i < nst) lds_read32(e, sg0 + (uint32_t)(i * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+      if (i < nst) to_list((int)((uint32_t)e >> 26), e & 0x3ffffff);
+    }
+    nst = 0;
+  };
   // results of tile tt (computed in the following tile's shadow) -> HBM; (a0, a1, inv): tile tt's
   // accumulators and 1/||x|| (UREC)
   auto flush = [&](int tt, const v16i& a0, const v16i& a1, float inv) {
     const int lr = tstart(tt) + r;
     const bool ok = lane_valid(tt);
     if constexpr (!DENSE) {
-      if (__ballot(umax >= 0.f)) {  // rare: ~k * n / sample rows per query over the corpus
-        uint32_t m = 0;
-        static_for<0, NE>([&](auto E) {
-          constexpr int e = decltype(E)::value;
-          if constexpr (UREC)
-            m |= (uval(a0, a1, e, inv) >= 0.f ? 1u : 0u) << e;
-          else
-            m |= (ures[e] >= 0.f ? 1u : 0u) << e;
-        });
+      if (!(VRQ_G5_BISECT & 16) && __ballot(SEED2 ? imax >= 0 : HMASK ? hm != 0 : umax >= 0.f)) {
+        uint32_t m = 0;  // (hits: ~k * n / sample rows per query over the corpus)
+        if constexpr (SEED2) {
+          static_for<0, KNE>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            m |= (((e >> 4) ? a1 : a0)[e & 15] >= 0 ? 1u : 0u) << (KNE - 1 - e);
+          });
+        } else if constexpr (HMASK) {
+          m = hm;
+        } else {
+          static_for<0, KNE>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            if constexpr (UREC)
+              m |= (uval(a0, a1, e, inv) >= 0.f ? 1u : 0u) << (KNE - 1 - e);
+            else
+              m |= (ures[e] >= 0.f ? 1u : 0u) << (KNE - 1 - e);
+          });
+        }
         if (!ok) m = 0;
-        while (m) {
-          const int e = __builtin_ctz(m);
-          m &= m - 1;
-          const int ql = qrow(e);  // list position from this wave's LDS counter
-          int pos;
-          lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
-          if (pos < capc) cand[(int64_t)(qbase + ql) * qstride + (int64_t)chunk * capc + pos] = (uint32_t)(row0 + lr);
+        if (STAGE && !__ballot((m & (m - 1)) != 0)) {
+          // at most one hit per lane: one staged entry per hit lane at its rank among them
+          const uint64_t lanes = __ballot(m != 0);
+          if (m) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0));
+            const int ql = qrow(KNE - 1 - __builtin_ctz(m));
+            lds_write32(sg0 + (uint32_t)((nst + below) * 4), (int)(((uint32_t)ql << 26) | (uint32_t)lr));
+          }
+          nst += __popcll(lanes);
+          if (nst > STG5 - 64) drain();  // (rare: >= STG5 - 64 hits in one chunk)
+        } else {
+          while (m) {  // several hits in a lane: straight to the lists
+            const int e = KNE - 1 - __builtin_ctz(m);
+            m &= m - 1;
+            to_list(qrow(e), lr);
+          }
         }
       }
       umax = -__builtin_inff();
+      hm = 0;
+      imax = INT32_MIN;
     }
+  };
+  // SEED2 test of accumulator register e of the tested tile (pairs fold into one v_max3_i32)
+  auto itest = [&](const v16i& a0, const v16i& a1, int e) {
+    const int v = ((e >> 4) ? a1 : a0)[e & 15];
+    if (e & 1)
+      imax = max(imax, max(iodd, v));
+    else
+      iodd = v;
   };
   // the sample pass keeps, per (lane, test), the running max of u over the chunk's rows of that
   // lane (NaN: none yet; rows already seen in the previous tile, and Phase-III zero norms, are NaN
@@ -490,6 +589,8 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   auto test = [&](float u, int e, bool vp) {
     if constexpr (DENSE) {
       ures[e] = fmaxf(ures[e], vp ? u : __builtin_nanf(""));
+    } else if constexpr (HMASK) {
+      hm = (hm << 1) | (u >= 0.f ? 1u : 0u);  // NaN: no hit
     } else if constexpr (UREC) {
       if (e & 1)
         umax = fmaxf(umax, fmaxf(uodd, u));  // pairs fold into one v_max3
@@ -584,13 +685,21 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(GKS - 1 - s) : "memory");
       }
       if constexpr (!(VRQ_G5_BISECT & 8)) {
-        acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
-        acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
+        if constexpr (SEED2) {  // tile starts at -ceil(thr) (Phase II, one piece: two M-blocks)
+          acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? seed[0] : acc[p][0]);
+          acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? seed[SEED2 ? 1 : 0] : acc[p][1]);
+        } else {
+          acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
+          if constexpr (NA == 2) acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
+        }
       } else if constexpr (s == 0) {
         acc[p][0] = ring[0].x + zero;
-        acc[p][1] = ring[0].y + zero;
+        if constexpr (NA == 2) acc[p][1] = ring[0].y + zero;
       }
-      asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
+      if constexpr (NA == 2)
+        asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
+      else
+        asm volatile("" : "+v"(acc[p][0]));
       // DMA of tile t + AHEAD, spread over the MFMA shadow
       if constexpr (RS) {
         // piece i at k-step 2 + DS*i: write staged row i of tile t+1 (loaded during tile t-1; the 8
@@ -612,7 +721,7 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
           if (ld) stage_load(t + 2, i);
         }
       } else if constexpr (P3) {
-        constexpr int DS = VRQ_G5_DMA_STRIDE, NPC3 = NREG ? 8 : 9;
+        constexpr int DS = VRQ_G5_DMA_STRIDE, NPC3 = NREG ? RPW : RPW + 1;
         if constexpr (s >= 2 && s < 2 + DS * NPC3 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2)) {
           if constexpr (NREG && s == 2)
             if (dma) issue_norm(t + AHEAD, nvr[p]);  // (nv holds this tile's norm already)
@@ -625,10 +734,15 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
         if constexpr (s >= 5 && s < 13) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
       }
       // threshold test / dense value of tile t-1, one per k-step in [EOFF, EOFF + NE)
-      constexpr int EOFF = NE == 16 ? 4 : 0;
-      if constexpr (s >= EOFF && s < EOFF + NE) {
+      constexpr int EOFF = KNE == 16 ? 4 : 0;
+      if constexpr (s >= EOFF && s < EOFF + KNE) {
         constexpr int e = s - EOFF;
-        if constexpr (!first && !(VRQ_G5_BISECT & 1)) test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e, vprev);
+        if constexpr (!first && !(VRQ_G5_BISECT & 1)) {
+          if constexpr (SEED2)
+            itest(acc[p ^ 1][0], acc[p ^ 1][1], e);
+          else
+            test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e, vprev);
+        }
       }
       if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
         invc = (nv > 0.0 && lane_valid(t)) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
@@ -661,11 +775,19 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
   }
   const bool vlast = lane_valid(ntiles - 1);
 #pragma unroll
-  for (int e = 0; e < NE; ++e)
-    test(pl ? uval(acc[1][0], acc[1][1], e, invp) : uval(acc[0][0], acc[0][1], e, invp), e, vlast);
+  for (int e = 0; e < KNE; ++e) {
+    if constexpr (SEED2) {
+      if (pl)
+        itest(acc[1][0], acc[1][1], e);
+      else
+        itest(acc[0][0], acc[0][1], e);
+    } else {
+      test(pl ? uval(acc[1][0], acc[1][1], e, invp) : uval(acc[0][0], acc[0][1], e, invp), e, vlast);
+    }
+  }
   if constexpr (DENSE) {  // the lane maxima of the chunk -> dv[q][chunk * 32 + r]
 #pragma unroll
-    for (int e = 0; e < NE; ++e) {
+    for (int e = 0; e < KNE; ++e) {
       const int q = qbase + qrow(e);
       if (q < nq) dv[(int64_t)q * dv_stride + (int64_t)chunk * GRT + r] = ures[e];
     }
@@ -675,8 +797,9 @@ __global__ __launch_bounds__(GW * 64, 1) void gemm_topk_kernel(
     flush(ntiles - 1, acc[0][0], acc[0][1], invp);
   }
   if constexpr (!DENSE) {
+    if constexpr (STAGE) drain();
     wait_lgkm0();
-    if (l < GQW && qbase + l < nq) ccnt[(int64_t)(qbase + l) * nchunks + chunk] = lcnt[w * GQW + l];
+    if (l < KQW && qbase + l < nq) ccnt[(int64_t)(qbase + l) * nchunks + chunk] = lcnt[w * KQW + l];
   }
 }
 
@@ -1185,7 +1308,7 @@ void launch_finish(const Rows& c, const uint8_t* src, int64_t n, int64_t row_off
   hipLaunchKernelGGL((gemm_finish_kernel<PH, false>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
                      (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
                      flag, thr, alpha, beta, delta, qbf);
-  hipLaunchKernelGGL((gemm_topk_kernel<MP, false, true>), dim3(p.nchunks * p.nqb), dim3(GW * 64), 0, s, src, c.norms, n, qa,
+  hipLaunchKernelGGL((gemm_topk_kernel<MP, false, true>), dim3(p.nchunks * p.nqb), dim3(KShape<MP>::W * 64), 0, s, src, c.norms, n, qa,
                      nq, (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
                      (float*)nullptr, (int64_t)0, (const int32_t*)qbf);
   hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
@@ -1221,7 +1344,7 @@ int gemm_run(int mode, const Rows& c, const double* bounds, int64_t n, int64_t r
   const bool P3 = mode != VRQ_GEMM_BINARY;  // int8 rows on the matrix cores
   const uint8_t* src = P3 ? (const uint8_t*)c.x8 : c.codes;
   const double* rn = c.norms;
-  const dim3 blk(GW * 64);
+  const dim3 blk(P3 ? KShape<VRQ_GEMM_INT8_COSINE>::W * 64 : KShape<VRQ_GEMM_BINARY>::W * 64);
   if (st & VRQ_GEMM_STAGE_SAMPLE) {
     hipLaunchKernelGGL(gemm_prep_kernel, dim3((p.nq_pad + 3) / 4), dim3(256), 0, s, mode, qf, nq, p.nq_pad, qa,
                        delta, alpha, beta, bounds);
