@@ -386,16 +386,17 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
     float scale = gscale;
     bool flat = false;
     if constexpr (MODE == VRQ_ENC_INT4_GLOBAL || MODE == VRQ_ENC_INT8_LOCAL || MODE == VRQ_ENC_INT4_LOCAL) {
+      // min / max as v_med3 against -+inf (no NaN canonicalisation per element)
       float mn = e[0], mx = e[0];
 #pragma unroll
       for (int i = 1; i < 16; ++i) {
-        mn = fminf(mn, e[i]);
-        mx = fmaxf(mx, e[i]);
+        mn = __builtin_amdgcn_fmed3f(mn, e[i], -__builtin_inff());
+        mx = __builtin_amdgcn_fmed3f(mx, e[i], __builtin_inff());
       }
 #pragma unroll
       for (int m = 1; m < WAVE; m <<= 1) {
-        mn = fminf(mn, __shfl_xor(mn, m, WAVE));
-        mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
+        mn = __builtin_amdgcn_fmed3f(mn, __shfl_xor(mn, m, WAVE), -__builtin_inff());
+        mx = __builtin_amdgcn_fmed3f(mx, __shfl_xor(mx, m, WAVE), __builtin_inff());
       }
       if constexpr (MODE != VRQ_ENC_INT4_GLOBAL) {
         if (l == 0) {
@@ -411,22 +412,27 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
     for (int k = 0; k < 4; ++k) {
       const float* ek = e + 4 * k;
       const int64_t o = v * 1024 + 256 * k + 4 * l;  // element index of ek[0]
+      // (clamps as v_med3 -- no NaN canonicalisation; round half to even = v_rndne; integer-valued
+      // results are packed by v_cvt_pk_u8_f32 after a +128 / +8 bias, which is exact for them)
       if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
         uint32_t wd = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float y = clampf(rintf(clampf(ek[c], -lim, lim) * scale), -127.f, 127.f);
-          wd |= ((uint32_t)(uint8_t)(int8_t)(int)y) << (8 * c);
+          const float y = __builtin_amdgcn_fmed3f(
+              __builtin_rintf(__builtin_amdgcn_fmed3f(ek[c], -lim, lim) * scale), -127.f, 127.f);
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(y + 128.f, c, wd);
         }
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + o) = wd;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + o) = wd ^ 0x80808080u;  // biased -> int8
       } else if constexpr (MODE == VRQ_ENC_INT16_GLOBAL) {
-        uint32_t wd[2] = {0, 0};
+        int y[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float y = clampf(rintf(clampf(ek[c], -lim, lim) * scale), -32767.f, 32767.f);
-          wd[c >> 1] |= ((uint32_t)(uint16_t)(int16_t)(int)y) << (16 * (c & 1));
-        }
-        *reinterpret_cast<uint2*>(reinterpret_cast<int16_t*>(qout) + o) = make_uint2(wd[0], wd[1]);
+        for (int c = 0; c < 4; ++c)
+          y[c] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_amdgcn_fmed3f(ek[c], -lim, lim) * scale),
+                                              -32767.f, 32767.f);
+        typedef short s2v __attribute__((ext_vector_type(2)));
+        const s2v lo = __builtin_amdgcn_cvt_pk_i16(y[0], y[1]), hi = __builtin_amdgcn_cvt_pk_i16(y[2], y[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<int16_t*>(qout) + o) =
+            make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
       } else if constexpr (MODE == VRQ_ENC_INT8_LOCAL) {
         uint32_t wd = 0;
 #pragma unroll
@@ -436,17 +442,14 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
         }
         *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(qout) + o) = wd;
       } else {  // int4: nibble pairs, high = even index; bytes (o / 2), (o / 2) + 1
-        uint32_t hw = 0;
+        uint32_t bw = 0;  // biased values 0..15 of elements c = 0..3 in bytes 0..3
 #pragma unroll
-        for (int c = 0; c < 4; c += 2) {
-          uint32_t byte4 = 0;
-          if (!flat) {
-            const int a = (int)clampf(rintf(ek[c] * scale), -8.f, 7.f) + 8;
-            const int b = (int)clampf(rintf(ek[c + 1] * scale), -8.f, 7.f) + 8;
-            byte4 = (uint32_t)(((a & 0x0f) << 4) | (b & 0x0f));
-          }
-          hw |= byte4 << (4 * c);
-        }
+        for (int c = 0; c < 4; ++c)
+          bw = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(ek[c] * scale), -8.f, 7.f) + 8.f,
+                                              c, bw);
+        // bytes (a0, b0, a1, b1) -> (a0 << 4 | b0, a1 << 4 | b1)
+        const uint32_t t = ((bw & 0x00ff00ffu) << 4) | ((bw >> 8) & 0x00ff00ffu);
+        const uint32_t hw = flat ? 0u : ((t & 0xffu) | ((t >> 8) & 0xff00u));
         *reinterpret_cast<uint16_t*>(reinterpret_cast<int8_t*>(qout) + o / 2) = (uint16_t)hw;
       }
     }

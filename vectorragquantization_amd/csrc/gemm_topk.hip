@@ -979,7 +979,7 @@ constexpr int kScoreBatch =
 // running list in order.  All threads of the block call it; returns kc = min(k, count).
 template <int PH, class RowAt>
 __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const Rows& c, int k,
-                            uint64_t* key, uint32_t* row, int32_t* fill) {
+                            uint64_t* key, uint32_t* row, int32_t* fill, uint32_t* bid = nullptr) {
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
   if (tid == 0) *fill = 0;
   int kc = 0;
@@ -989,11 +989,15 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
     const uint32_t kr = kc == k ? row[k - 1] : 0xffffffffu;
     const int64_t end = base + FB_BATCH < count ? base + FB_BATCH : count;
     constexpr int U = kScoreBatch<PH>;
+    if (bid) {  // the batch's row ids -> LDS by all threads at once (row_at may read global memory)
+      for (int64_t j = base + tid; j < end; j += 256) bid[j - base] = row_at(j);
+      __syncthreads();
+    }
     for (int64_t j0 = base + w; j0 < end; j0 += 4 * U) {  // this wave: j0, j0 + 4, ... (wave-uniform)
       uint32_t rr[U];
       RowSlice<PH> d[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) rr[u] = j0 + 4 * u < end ? row_at(j0 + 4 * u) : 0u;
+      for (int u = 0; u < U; ++u) rr[u] = j0 + 4 * u < end ? (bid ? bid[j0 + 4 * u - base] : row_at(j0 + 4 * u)) : 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (j0 + 4 * u < end) d[u] = load_row<PH>(c, (int64_t)rr[u]);
@@ -1031,6 +1035,7 @@ constexpr int MAX_CHUNKS = 2048;  // per-query candidate lists the finish kernel
 struct FinShared {
   uint64_t key[KMAX5 + FB_BATCH];
   uint32_t row[KMAX5 + FB_BATCH];
+  uint32_t bid[FB_BATCH];       // the current batch's candidate rows
   int32_t pre[MAX_CHUNKS + 1];  // exclusive prefix of the list lengths
   int32_t misc[4];
 };
@@ -1065,16 +1070,44 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   if (tid == 0) sh.misc[1] = 0;  // overflow
   __syncthreads();
   const int32_t* cq = ccnt + (int64_t)q * nchunks;
-  for (int c = tid; c < nchunks; c += 256)
-    if (cq[c] > capc) atomicOr(&sh.misc[1], 1);
-  if (tid == 0) {
-    int acc = 0;
-    for (int c = 0; c < nchunks; ++c) {
-      sh.pre[c] = acc;
-      const int v = cq[c];
-      acc += v < capc ? v : capc;
+  // exclusive prefix of the (capped) list lengths: thread t owns chunks [t * per, t * per + per),
+  // all its loads in flight at once, then a block scan of the 256 partial sums (a serial loop over
+  // the chunks cost one dependent global load per chunk)
+  {
+    constexpr int PER_MAX = (MAX_CHUNKS + 255) / 256;
+    const int per = (nchunks + 255) / 256, c0 = tid * per;
+    int v[PER_MAX];
+    int part = 0;
+#pragma unroll
+    for (int i = 0; i < PER_MAX; ++i) {
+      const int c = c0 + i;
+      const int x = (i < per && c < nchunks) ? cq[c] : 0;
+      if (x > capc) atomicOr(&sh.misc[1], 1);
+      v[i] = x < capc ? x : capc;
+      part += v[i];
     }
-    sh.pre[nchunks] = acc;
+    // inclusive scan of `part` over the block: wave scan (shuffles), then the 4 wave totals
+    int incl = part;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const int y = __shfl_up(incl, d, WAVE);
+      if (lane_id() >= d) incl += y;
+    }
+    __shared__ int wtot[4];
+    if (lane_id() == WAVE - 1) wtot[tid >> 6] = incl;
+    __syncthreads();
+    int off = 0;
+    for (int ww = 0; ww < (tid >> 6); ++ww) off += wtot[ww];
+    int acc = off + incl - part;  // exclusive prefix of this thread's first chunk
+#pragma unroll
+    for (int i = 0; i < PER_MAX; ++i) {
+      const int c = c0 + i;
+      if (i < per && c < nchunks) {
+        sh.pre[c] = acc;
+        acc += v[i];
+      }
+    }
+    if (tid == 255) sh.pre[nchunks] = wtot[0] + wtot[1] + wtot[2] + wtot[3];
   }
   __syncthreads();
   const int total = sh.pre[nchunks];
@@ -1104,7 +1137,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   };
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  const int kc = running_topk<PH>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2]);
+  const int kc = running_topk<PH>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2], sh.bid);
   if (!RETRY && sh.misc[1]) {  // overflow: raise the threshold to the recorded k-th score, retry
     if (tid == 0) {
       const double sk = desc_key_inv(sh.key[kc - 1]);
