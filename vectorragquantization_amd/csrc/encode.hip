@@ -308,6 +308,45 @@ constexpr int ENC_WPB = 4;                       // waves per workgroup (each on
 constexpr bool kEncPersist = VRQ_ENC_WGS_PER_CU > 0;
 constexpr int ENC_SLICE = 1024 + 64;             // floats per wave slice (+ padding)
 
+// One butterfly step without the LDS crossbar (a __shfl_xor is a ds_bpermute round trip, ~100+
+// cycles on the wave's critical path): lane l combines its value with lane l ^ M's.  M = 1, 2: quad
+// DPP; M = 4, 8: the half-row / row mirror DPP, which pair lane l with a lane of the group l ^ M
+// once every group of M lanes holds a single value (true after the steps below M); M = 16, 32:
+// v_permlane16/32_swap, which hand every lane both values of the pair.  OP is commutative, so each
+// lane computes the same value as OP(own, partner) of the __shfl_xor butterfly (bit-exact).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+template <int M, class OP>
+__device__ __forceinline__ float bfly(float x, OP op) {
+  if constexpr (M == 1) {
+    return op(x, dpp_mov<0xB1>(x));  // quad_perm [1,0,3,2]
+  } else if constexpr (M == 2) {
+    return op(x, dpp_mov<0x4E>(x));  // quad_perm [2,3,0,1]
+  } else if constexpr (M == 4) {
+    return op(x, dpp_mov<0x141>(x));  // row_half_mirror
+  } else if constexpr (M == 8) {
+    return op(x, dpp_mov<0x140>(x));  // row_mirror
+  } else if constexpr (M == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return op(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  } else {
+    static_assert(M == 32, "butterfly step");
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return op(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  }
+}
+template <class OP>
+__device__ __forceinline__ float wave_allreduce(float x, OP op) {
+  x = bfly<1>(x, op);
+  x = bfly<2>(x, op);
+  x = bfly<4>(x, op);
+  x = bfly<8>(x, op);
+  x = bfly<16>(x, op);
+  return bfly<32>(x, op);
+}
+
 template <int MODE>
 __device__ __forceinline__ void enc1024_load(float4 (&x)[4], const float* __restrict__ row, int l) {
 #pragma unroll
@@ -358,12 +397,7 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
       float r = leaf[0];
 #pragma unroll
       for (int i = 1; i < 16; ++i) r += leaf[8 * i];
-      r = r + __shfl_xor(r, 1, WAVE);
-      r = r + __shfl_xor(r, 2, WAVE);
-      r = r + __shfl_xor(r, 4, WAVE);
-      r = r + __shfl_xor(r, 8, WAVE);
-      r = r + __shfl_xor(r, 16, WAVE);
-      r = r + __shfl_xor(r, 32, WAVE);
+      r = wave_allreduce(r, [](float a, float b) { return a + b; });
       mean = (float)((double)r / 1024.0);  // np.float32(sum) / np.intp(n) -> float32
     }
     // code bytes 2l, 2l+1 = elements 16l..16l+15 (MSB first)
@@ -393,11 +427,8 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
         mn = __builtin_amdgcn_fmed3f(mn, e[i], -__builtin_inff());
         mx = __builtin_amdgcn_fmed3f(mx, e[i], __builtin_inff());
       }
-#pragma unroll
-      for (int m = 1; m < WAVE; m <<= 1) {
-        mn = __builtin_amdgcn_fmed3f(mn, __shfl_xor(mn, m, WAVE), -__builtin_inff());
-        mx = __builtin_amdgcn_fmed3f(mx, __shfl_xor(mx, m, WAVE), __builtin_inff());
-      }
+      mn = wave_allreduce(mn, [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); });
+      mx = wave_allreduce(mx, [](float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); });
       if constexpr (MODE != VRQ_ENC_INT4_GLOBAL) {
         if (l == 0) {
           minmax[2 * v] = (double)mn;
