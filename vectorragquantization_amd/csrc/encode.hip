@@ -347,10 +347,24 @@ __device__ __forceinline__ float wave_allreduce(float x, OP op) {
   return bfly<32>(x, op);
 }
 
+#ifndef VRQ_ENC_NT
+#define VRQ_ENC_NT 0  // probe builds: 1 = the input rows by non-temporal loads (read once)
+#endif
+#ifndef VRQ_ENC_LATE
+#define VRQ_ENC_LATE 0  // probe builds: 1 = the global modes quantise after the mean (no early stores)
+#endif
 template <int MODE>
 __device__ __forceinline__ void enc1024_load(float4 (&x)[4], const float* __restrict__ row, int l) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) x[k] = *reinterpret_cast<const float4*>(row + 256 * k + 4 * l);
+  for (int k = 0; k < 4; ++k) {
+    if constexpr (VRQ_ENC_NT) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + 256 * k + 4 * l));
+      x[k] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      x[k] = *reinterpret_cast<const float4*>(row + 256 * k + 4 * l);
+    }
+  }
 }
 
 template <int MODE>
@@ -416,6 +430,10 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
         }
       }
       *reinterpret_cast<uint16_t*>(codes + v * 128 + 2 * l) = (uint16_t)bits;
+    }
+    if constexpr (VRQ_ENC_LATE) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e[i]) : "v"(mean));
     }
     float scale = gscale;
     bool flat = false;

@@ -89,6 +89,10 @@ constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave <
 #endif
 // Phase-III thresholded pass: stage the int8 tiles through registers (global_load_dwordx4 during
 // tile t-1, ds_write_b128 into the image during tile t, for tile t+1) instead of LDS-DMA
+// cache policy (aux bits) of the corpus-row LDS-DMA pieces (probe builds: 2 = non-temporal)
+#ifndef VRQ_G5_DMA_AUX
+#define VRQ_G5_DMA_AUX 0
+#endif
 #ifndef VRQ_G5_REGSTAGE
 #define VRQ_G5_REGSTAGE 0
 #endif
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sink) : "v"(g) : "memory");
       asm volatile("" ::"v"(sink));
     } else {
-      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, VRQ_G5_DMA_AUX);
     }
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
