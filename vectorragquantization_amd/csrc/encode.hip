@@ -347,17 +347,26 @@ __device__ __forceinline__ float wave_allreduce(float x, OP op) {
   return bfly<32>(x, op);
 }
 
+// Input rows by non-temporal loads (each f32 row is read once) for the modes where that measured
+// faster: int8g 0.66 -> 0.71, int16g 0.70 -> 0.71, Cohere 0.71 -> 0.72 of HBM; int4g and the local
+// modes measured 0.01-0.02 slower with it (tools/enc_probe.py, profiles/r3_encode_nt_variants.jsonl).
+// VRQ_ENC_NT (probe builds): 0 none, 1 every mode, 2 = this selection (the library default).
 #ifndef VRQ_ENC_NT
-#define VRQ_ENC_NT 0  // probe builds: 1 = the input rows by non-temporal loads (read once)
+#define VRQ_ENC_NT 2
 #endif
 #ifndef VRQ_ENC_LATE
 #define VRQ_ENC_LATE 0  // probe builds: 1 = the global modes quantise after the mean (no early stores)
 #endif
 template <int MODE>
+constexpr bool enc_nt() {
+  return VRQ_ENC_NT == 1 ||
+         (VRQ_ENC_NT == 2 && (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_INT16_GLOBAL || MODE == VRQ_ENC_COHERE));
+}
+template <int MODE>
 __device__ __forceinline__ void enc1024_load(float4 (&x)[4], const float* __restrict__ row, int l) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if constexpr (VRQ_ENC_NT) {
+    if constexpr (enc_nt<MODE>()) {
       typedef float f4v __attribute__((ext_vector_type(4)));
       const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + 256 * k + 4 * l));
       x[k] = make_float4(v.x, v.y, v.z, v.w);
