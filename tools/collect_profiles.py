@@ -18,7 +18,8 @@ def main(rnd, src, overrides):
     for d in sorted(glob.glob(os.path.join(src, "c*_nq*"))):
         cfg, nq = os.path.basename(d).split("_nq")
         tag = f"{rnd}_{cfg}_n{rows[cfg]}_nq{nq}_g1"
-        stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
+        stats = glob.glob(os.path.join(d, "kernel_stats.csv")) or \
+            glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
         if stats:
             shutil.copy(stats[0], os.path.join(here, "profiles", f"{tag}_kernel_stats.csv"))
         summ = os.path.join(d, "summary.json")

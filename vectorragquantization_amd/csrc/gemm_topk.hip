@@ -89,6 +89,10 @@ constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave <
 #endif
 // Phase-III thresholded pass: stage the int8 tiles through registers (global_load_dwordx4 during
 // tile t-1, ds_write_b128 into the image during tile t, for tile t+1) instead of LDS-DMA
+// threshold tests held at their k-steps by a register pin (0: probe builds, the compiler's placement)
+#ifndef VRQ_G5_PIN_TESTS
+#define VRQ_G5_PIN_TESTS 1
+#endif
 // cache policy (aux bits) of the corpus-row LDS-DMA pieces (probe builds: 2 = non-temporal)
 #ifndef VRQ_G5_DMA_AUX
 #define VRQ_G5_DMA_AUX 0
@@ -746,10 +750,28 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
             itest(acc[p ^ 1][0], acc[p ^ 1][1], e);
           else
             test(uval(acc[p ^ 1][0], acc[p ^ 1][1], e, invp), e, vprev);
+          // pin the test's running state at this k-step: the tests are pure arithmetic, and without
+          // a use here IR-level sinking gathers all of them after the tile's last MFMAs (past the
+          // norm branch at s = 20), one ~90-instruction burst per tile instead of a few instructions
+          // in each MFMA gap
+          if constexpr (VRQ_G5_PIN_TESTS) {
+            if constexpr (SEED2)
+              asm volatile("" : "+v"(imax), "+v"(iodd));
+            else if constexpr (DENSE)
+              asm volatile("" : "+v"(ures[e]));
+            else if constexpr (HMASK)
+              asm volatile("" : "+v"(hm));
+            else if constexpr (UREC)
+              asm volatile("" : "+v"(umax), "+v"(uodd));
+            else
+              asm volatile("" : "+v"(ures[e]), "+v"(umax));
+          }
         }
       }
       if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
-        invc = (nv > 0.0 && lane_valid(t)) ? __builtin_amdgcn_rcpf((float)nv) : __builtin_nanf("");
+        // (branch-free: a short-circuit && here splits the tile's basic block and its schedule)
+        const float rc = __builtin_amdgcn_rcpf((float)nv);
+        invc = ((nv > 0.0) & lane_valid(t)) ? rc : __builtin_nanf("");
       }
       VRQ_SCHED_FENCE();
     });
