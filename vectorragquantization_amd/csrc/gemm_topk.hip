@@ -1003,9 +1003,10 @@ constexpr int kScoreBatch =
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
 // (score desc, row asc), so the sort runs rarely once the list is full.  key/row[0..kc) hold the
 // running list in order.  All threads of the block call it; returns kc = min(k, count).
-template <int PH, class RowAt>
+template <int PH, int NW = 4, class RowAt>
 __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const Rows& c, int k,
                             uint64_t* key, uint32_t* row, int32_t* fill, uint32_t* bid = nullptr) {
+  constexpr int NT = NW * WAVE;
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
   if (tid == 0) *fill = 0;
   int kc = 0;
@@ -1016,20 +1017,20 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
     const int64_t end = base + FB_BATCH < count ? base + FB_BATCH : count;
     constexpr int U = kScoreBatch<PH>;
     if (bid) {  // the batch's row ids -> LDS by all threads at once (row_at may read global memory)
-      for (int64_t j = base + tid; j < end; j += 256) bid[j - base] = row_at(j);
+      for (int64_t j = base + tid; j < end; j += NT) bid[j - base] = row_at(j);
       __syncthreads();
     }
-    for (int64_t j0 = base + w; j0 < end; j0 += 4 * U) {  // this wave: j0, j0 + 4, ... (wave-uniform)
+    for (int64_t j0 = base + w; j0 < end; j0 += NW * U) {  // this wave: j0, j0 + NW, ... (wave-uniform)
       uint32_t rr[U];
       RowSlice<PH> d[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) rr[u] = j0 + 4 * u < end ? (bid ? bid[j0 + 4 * u - base] : row_at(j0 + 4 * u)) : 0u;
+      for (int u = 0; u < U; ++u) rr[u] = j0 + NW * u < end ? (bid ? bid[j0 + NW * u - base] : row_at(j0 + NW * u)) : 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (j0 + 4 * u < end) d[u] = load_row<PH>(c, (int64_t)rr[u]);
+        if (j0 + NW * u < end) d[u] = load_row<PH>(c, (int64_t)rr[u]);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (j0 + 4 * u >= end) break;
+        if (j0 + NW * u >= end) break;
         const uint64_t key_r = desc_key_f64(score_row<PH>(qv, d[u]));
         const bool take = kc < k || key_r < kk || (key_r == kk && rr[u] < kr);
         if (take && l == 0) {
@@ -1044,7 +1045,7 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
     if (f > 0) {
       const int tot = kc + f;
       const int np2 = next_pow2(tot);
-      for (int i = tot + tid; i < np2; i += 256) {
+      for (int i = tot + tid; i < np2; i += NT) {
         key[i] = KEY_NONE;
         row[i] = 0xffffffffu;
       }
@@ -1058,6 +1059,14 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
 }
 
 constexpr int MAX_CHUNKS = 2048;  // per-query candidate lists the finish kernel indexes
+// finish: threads per query (one workgroup each).  Measured at 10M rows, nq = 1024 (~1.8K Phase-III /
+// ~1.3K Phase-II candidates per query, evenly spread: p99 / mean 1.2-1.4, tools/c5_candidates.py):
+// 256 threads 0.86 / 0.51 ms, 512 threads 0.80 / 0.47 ms, 1024 threads 0.93 / 0.58 ms (Phase III /
+// Phase II; profiles/r3_c5_finish_variants.jsonl).  VRQ_G5_FIN_NT overrides it in probe builds.
+#ifndef VRQ_G5_FIN_NT
+#define VRQ_G5_FIN_NT 512
+#endif
+constexpr int FIN_NT = VRQ_G5_FIN_NT, FIN_NW = FIN_NT / WAVE;
 struct FinShared {
   uint64_t key[KMAX5 + FB_BATCH];
   uint32_t row[KMAX5 + FB_BATCH];
@@ -1078,7 +1087,7 @@ struct FinShared {
 // goes to the fallback.  A served or abandoned query's thr becomes +inf, so a retry pass over its
 // query block records nothing for it.
 template <int PH, bool RETRY>
-__global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t n,
+__global__ __launch_bounds__(FIN_NT) void gemm_finish_kernel(const Rows c, int64_t n,
                                                           int64_t row_offset, const float* __restrict__ qf, int k,
                                                           const uint32_t* __restrict__ cand,
                                                           const int32_t* __restrict__ ccnt, int nchunks, int capc,
@@ -1097,11 +1106,11 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   __syncthreads();
   const int32_t* cq = ccnt + (int64_t)q * nchunks;
   // exclusive prefix of the (capped) list lengths: thread t owns chunks [t * per, t * per + per),
-  // all its loads in flight at once, then a block scan of the 256 partial sums (a serial loop over
+  // all its loads in flight at once, then a block scan of the FIN_NT partial sums (a serial loop over
   // the chunks cost one dependent global load per chunk)
   {
-    constexpr int PER_MAX = (MAX_CHUNKS + 255) / 256;
-    const int per = (nchunks + 255) / 256, c0 = tid * per;
+    constexpr int PER_MAX = (MAX_CHUNKS + FIN_NT - 1) / FIN_NT;
+    const int per = (nchunks + FIN_NT - 1) / FIN_NT, c0 = tid * per;
     int v[PER_MAX];
     int part = 0;
 #pragma unroll
@@ -1119,7 +1128,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
       const int y = __shfl_up(incl, d, WAVE);
       if (lane_id() >= d) incl += y;
     }
-    __shared__ int wtot[4];
+    __shared__ int wtot[FIN_NW];
     if (lane_id() == WAVE - 1) wtot[tid >> 6] = incl;
     __syncthreads();
     int off = 0;
@@ -1133,7 +1142,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
         acc += v[i];
       }
     }
-    if (tid == 255) sh.pre[nchunks] = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    if (tid == FIN_NT - 1) sh.pre[nchunks] = off + incl;
   }
   __syncthreads();
   const int total = sh.pre[nchunks];
@@ -1163,7 +1172,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
   };
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  const int kc = running_topk<PH>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2], sh.bid);
+  const int kc = running_topk<PH, FIN_NW>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2], sh.bid);
   if (!RETRY && sh.misc[1]) {  // overflow: raise the threshold to the recorded k-th score, retry
     if (tid == 0) {
       const double sk = desc_key_inv(sh.key[kc - 1]);
@@ -1174,7 +1183,7 @@ __global__ __launch_bounds__(256) void gemm_finish_kernel(const Rows c, int64_t 
     }
     return;
   }
-  for (int i = tid; i < k; i += 256) {
+  for (int i = tid; i < k; i += FIN_NT) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)sh.row[i] + row_offset : -1;
     out_scores[o] = i < kc ? desc_key_inv(sh.key[i]) : __builtin_nan("");
@@ -1364,13 +1373,13 @@ void launch_finish(const Rows& c, const uint8_t* src, int64_t n, int64_t row_off
                    int64_t* out_rows, double* out_scores, int32_t* flag, const double* alpha, const double* beta,
                    const double* delta, int32_t* qbf, bool fb, hipStream_t s) {
   constexpr int MP = PH == VRQ_GEMM_BINARY ? VRQ_GEMM_BINARY : VRQ_GEMM_INT8_COSINE;  // matrix-pass kind
-  hipLaunchKernelGGL((gemm_finish_kernel<PH, false>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
+  hipLaunchKernelGGL((gemm_finish_kernel<PH, false>), dim3(nq), dim3(FIN_NT), 0, s, c, n, row_offset, qf, k,
                      (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
                      flag, thr, alpha, beta, delta, qbf);
   hipLaunchKernelGGL((gemm_topk_kernel<MP, false, true>), dim3(p.nchunks * p.nqb), dim3(KShape<MP>::W * 64), 0, s, src, c.norms, n, qa,
                      nq, (const float*)thr, cand, cnt, p.capc, p.chunk_rows, p.chunk_rows, p.nchunks, p.nqb,
                      (float*)nullptr, (int64_t)0, (const int32_t*)qbf);
-  hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k,
+  hipLaunchKernelGGL((gemm_finish_kernel<PH, true>), dim3(nq), dim3(FIN_NT), 0, s, c, n, row_offset, qf, k,
                      (const uint32_t*)cand, (const int32_t*)cnt, p.nchunks, p.capc, out_count, out_rows, out_scores,
                      flag, thr, alpha, beta, delta, qbf);
   hipLaunchKernelGGL(gemm_fallback_kernel<PH>, dim3(nq), dim3(256), 0, s, c, n, row_offset, qf, k, out_count,

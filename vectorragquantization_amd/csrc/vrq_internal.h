@@ -55,16 +55,74 @@ __device__ __forceinline__ double shfl_xor_f64(double v, int m) {
   return __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(v), m));
 }
 
+// Wave butterflies without the LDS crossbar.  A __shfl_xor is a ds_bpermute round trip (~100+ cycles
+// on the wave's critical path, twice for 64-bit values); here lane l meets lane l ^ M through
+//   M = 1, 2: quad_perm DPP;
+//   M = 4, 8: the half-row / row mirror DPP, which pair lane l with a lane of the group l ^ M -- the
+//             same value once every group of M lanes holds a single value, which the steps below M
+//             establish for a commutative combine;
+//   M = 16, 32: v_permlane16/32_swap, which hand every lane both values of its pair.
+// Each lane then computes OP(own, partner) or OP(partner, own); for a commutative OP that is the
+// value the __shfl_xor butterfly computes, bit for bit.  VRQ_WAVE_SUM_DPP=0 (probe builds) keeps
+// the __shfl_xor form.
+#ifndef VRQ_WAVE_SUM_DPP
+#define VRQ_WAVE_SUM_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+template <int M>
+__device__ __forceinline__ uint32_t dpp_partner_u32(uint32_t x) {
+  static_assert(M == 1 || M == 2 || M == 4 || M == 8, "DPP butterfly step");
+  return dpp_u32<M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 4 ? 0x141 : 0x140>(x);
+}
+// one butterfly step on a 64-bit value (T = double / int64_t), combined by OP
+template <int M, class T, class OP>
+__device__ __forceinline__ T bfly64(T v, OP op) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+  if constexpr (M <= 8) {
+    const uint64_t p = ((uint64_t)dpp_partner_u32<M>(hi) << 32) | dpp_partner_u32<M>(lo);
+    return op(v, __builtin_bit_cast(T, p));
+  } else {
+    const auto pl = M == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                            : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto ph = M == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                            : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const T a = __builtin_bit_cast(T, ((uint64_t)ph[0] << 32) | pl[0]);  // the pair's lower-group value
+    const T b = __builtin_bit_cast(T, ((uint64_t)ph[1] << 32) | pl[1]);  // ... and its upper-group value
+    return op(a, b);
+  }
+}
+template <class T, class OP>
+__device__ __forceinline__ T wave_allreduce64(T v, OP op) {
+  v = bfly64<1>(v, op);
+  v = bfly64<2>(v, op);
+  v = bfly64<4>(v, op);
+  v = bfly64<8>(v, op);
+  v = bfly64<16>(v, op);
+  return bfly64<32>(v, op);
+}
+
 // f64 wave sum (butterfly; identical result in every lane)
 __device__ __forceinline__ double wave_sum_f64(double v) {
+  if constexpr (VRQ_WAVE_SUM_DPP) {
+    return wave_allreduce64(v, [](double a, double b) { return a + b; });
+  } else {
 #pragma unroll
-  for (int m = 1; m < WAVE; m <<= 1) v += shfl_xor_f64(v, m);
-  return v;
+    for (int m = 1; m < WAVE; m <<= 1) v += shfl_xor_f64(v, m);
+    return v;
+  }
 }
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+  if constexpr (VRQ_WAVE_SUM_DPP) {
+    return wave_allreduce64(v, [](int64_t a, int64_t b) { return a + b; });
+  } else {
 #pragma unroll
-  for (int m = 1; m < WAVE; m <<= 1) v += (int64_t)shfl_xor_u64((uint64_t)v, m);
-  return v;
+    for (int m = 1; m < WAVE; m <<= 1) v += (int64_t)shfl_xor_u64((uint64_t)v, m);
+    return v;
+  }
 }
 
 // Sortable 64-bit image of a double for DESCENDING order: larger double -> smaller key.
