@@ -36,7 +36,10 @@ constexpr int64_t kMfmaMinSample = 131072;  // (the sample pass writes lane mini
 constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~0.3 ms of MFMA at nq = 1024)
 constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
 constexpr int kMfmaMinQueries = 1;       // auto-selection threshold on the batch size (K1r below 129)
-constexpr int64_t kMfmaSampleDiv = 16;   // dense threshold sample = n / kMfmaSampleDiv rows
+// dense threshold sample = n / kMfmaSampleDiv rows (clamped above).  Per-step time at nq = 1024
+// (profiles/r3_c4_shard_sample_div.txt): 12.5M rows (one rank of 8) div 16 / 32 / 64 / 128 = 4.31 /
+// 4.22 / 4.23 / 4.32 ms, 25M rows 8.00 / 7.96 / 7.90 / 8.11 ms; 100M and 1M rows are at the clamps
+constexpr int64_t kMfmaSampleDiv = 32;
 
 struct MfmaPlan {
   int64_t sample;            // dense sample rows (sample_chunks * sample_chunk_rows)
