@@ -42,10 +42,19 @@
 #endif
 // hit extraction of a flagged (M-block, n-block): 1 = per-lane 16-bit hit masks and one staged
 // entry per lane when no lane holds two hits (the usual case), the 16-ballot walk otherwise;
-// 0 = always the 16-ballot walk
+// 2 = the same with register-tagged seeds (below): the two-hit check is one ballot per register
+// folded by scalar carry-save ORs, and the hit's query row comes from its value's tag, not a mask;
+// 0 = always the 16-ballot walk.  Measured (profiles/r3_k1m_hit_tag_ab.txt): 1 beats 2 (c2 matrix
+// pass 0.39 vs 0.45 ms, c4 29.1 vs 29.6 ms), so 2 stays a probe-build option.
 #ifndef VRQ_HIT_FAST
 #define VRQ_HIT_FAST 1
 #endif
+// Register-tagged seeds (VRQ_HIT_FAST == 2, thresholded passes): accumulator register g starts at
+// tau'/2 - 1/4 + g/1024 instead of tau'/2.  The untagged accumulator A = <q,r> + tau'/2 and the
+// threshold pc(r)/2 are multiples of 1/2, so A - 1/4 + g/1024 > pc(r)/2  <=>  A > pc(r)/2 (every
+// test unchanged), all values stay exact in f32 (|A| < 2^11, steps of 2^-10), the largest register
+// of a lane carries its own index g = (int(1024 x) & 511) - 256, and dist - tau = floor(pc - 2x).
+constexpr bool kHitTag = VRQ_HIT_FAST == 2;
 
 namespace vrq {
 
@@ -334,7 +343,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int m = 0; m < MB; ++m)
     if (l < 32) {  // lane l writes [m][h = l >> 4][g = l & 15]
       const int g = l & 15, hh = l >> 4;
-      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh] +
+                       (kHitTag && !DENSE ? (float)g * (1.0f / 1024.0f) - 0.25f : 0.0f);
     }
   const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64);  // this lane half's 16 seeds of M-block 0
   auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
@@ -444,7 +454,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
           // acc = <q,r> + tau'/2 with tau' = tau(q) - pc(q), so pc(r) - 2 acc = dist - tau(q) in
           // [-1025, -1] for a hit (exact integers): no per-query value to fetch on this path
-          const int v = pc - (int)(2.0f * a[g]);
+          const int v = kHitTag ? (int)floorf((float)pc - 2.0f * a[g]) : pc - (int)(2.0f * a[g]);
           const int pos = nst + below < STG ? nst + below : STG;
           lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
         }
@@ -459,6 +469,35 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   auto block_hits_fast = [&](const v16f& a, int m, int pc, float hp, int rel7) __attribute__((always_inline)) {
     if constexpr (!VRQ_HIT_FAST) {
       block_hits(a, m, pc, hp, rel7);
+    } else if constexpr (kHitTag) {
+      // lanes with >= 1 hit (ones) and with >= 2 (twos): one ballot per register, scalar ORs
+      uint64_t ones = 0, twos = 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const uint64_t b = __ballot(a[g] > hp);
+        twos |= ones & b;
+        ones |= b;
+      }
+      if (twos) {  // some lane holds two or more hits (rare)
+        block_hits(a, m, pc, hp, rel7);
+      } else {
+        if ((ones >> l) & 1) {
+          const v16i b = __builtin_bit_cast(v16i, a);  // >= 0 patterns order like their floats
+          const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
+          const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
+          const float mx = __int_as_float(max(max(max(x0, x1), x2), max(max(x3, x4), b[15])));
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(ones >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ones, 0));
+          int lo = l;
+          asm volatile("" : "+v"(lo));
+          const int g = ((int)(mx * 1024.0f) & 511) - 256;  // the tag of the lane's single hit
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+          const int v = (int)floorf((float)pc - 2.0f * mx);
+          const int pos = nst + below < STG ? nst + below : STG;
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
+        }
+        nst += __popcll(ones);
+      }
     } else {
       uint32_t m16 = 0;
 #pragma unroll
@@ -842,7 +881,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
   for (int m = 0; m < MB; ++m)
     if (l < 32) {
       const int g = l & 15, hh = l >> 4;
-      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];  // (K1r: untagged)
     }
   const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), stg0 = lds_addr(stg);
   const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
