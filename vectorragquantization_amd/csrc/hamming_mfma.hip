@@ -779,7 +779,19 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 //   the row: 4 conflict-free ds_read_b128 through the tile swizzle), queries the same dword.
 // Same thresholds (sampled tau_s / exact re-run with tau_p), same per-(query, chunk) lists and
 // suffix merge as K1m; the hit path flushes synchronously (hits are rare at the sizes this serves).
-constexpr int NPR = 3;  // per-wave packed ring depth (tile t+2 in flight while tile t is read)
+// Workgroups per CU of the MB = 1 instance (VRQ_K1R_OCC, probe builds): 2 puts two waves on every
+// SIMD (each at <= 256 VGPR + AGPR, a ring of 2 tiles per wave so two workgroups fit the LDS), so one
+// wave's MFMAs run while the other waits on its tile or unpacks.  MB = 2 would spill at 256 registers
+// (its sample pass keeps 32 lane minima besides 64 accumulators) and MB = 4 needs the whole register
+// file: both keep one wave per SIMD.
+#ifndef VRQ_K1R_OCC
+#define VRQ_K1R_OCC 2
+#endif
+template <int MB>
+constexpr int k1r_occ() { return MB == 1 ? VRQ_K1R_OCC : 1; }
+template <int MB>
+constexpr int k1r_npr() { return k1r_occ<MB>() == 2 ? 2 : 3; }  // per-wave packed ring depth
+constexpr int NPR_MAX = 3;  // (tile t+NPR-1 in flight while tile t is read)
 // cache-policy bits of K1r's LDS-DMA: 2 = nt (each row is read by one wave once per batch).  c3
 // (100M rows, nq = 8): 2.11 -> 2.02 ms per pass, 0.76 -> 0.79 of HBM (profiles/r2s3/c3_k1r_nt.txt)
 #ifndef VRQ_K1R_AUX
@@ -788,12 +800,13 @@ constexpr int NPR = 3;  // per-wave packed ring depth (tile t+2 in flight while 
 template <int MB>
 struct RowsShape {
   static constexpr int QPW = 32 * MB;
+  static constexpr int NPR = k1r_npr<MB>();
   static constexpr int SMEM = MWAVES * (NPR * PKT + QPW * 8 + (STG + 1) * 4 + MB * 128);
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(SMEM * k1r_occ<MB>() <= 160 * 1024, "LDS budget");
 };
 
 template <int MODE, int MB>
-__global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
+__global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_kernel(
     const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
@@ -802,6 +815,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
   // c * chunk_stride + t * tile_stride (every tile whole), lane minima to dv[q][c * 32 + lane row]
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
   constexpr int QPW = RowsShape<MB>::QPW;
+  constexpr int NPR = RowsShape<MB>::NPR;
   if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
   __shared__ __attribute__((aligned(16))) uint8_t smem[RowsShape<MB>::SMEM];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -984,7 +998,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
     // the next n-block's tile: its DMA landed (tile boundary), and the ring slot of tile t+NPR-1 ...
     if (par == 1 && blk + 1 < nblk) {
       const int t1 = (blk + 1) >> 1;  // tile about to be read
-      const int last = t1 + NPR - 2 < ntiles ? t1 + NPR - 2 : ntiles - 1;  // last tile issued so far
+      const int last = t1 + NPR - 1 < ntiles ? t1 + NPR - 1 : ntiles - 1;  // last tile issued so far
       wait_tiles(last - t1);
     }
     const int lr = blk * 32 + ri;
@@ -1039,9 +1053,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_rows_kernel(
     // row popcount of this n-block (both halves) and its threshold for the next n-block's tests
     pprev = pcs + __shfl_xor(pcs, 32, 64);
     hpb = __float_as_int(0.5f * (float)(lr < nrows ? pprev : 0x40000000));
-    // a tile consumed: refill its ring slot (the DMA of tile t + NPR)
-    if (par == 1 && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3])::"memory");
+    // tile t = blk >> 1 consumed once its second n-block's rows are in registers (nxt, read during
+    // the first n-block and complete here): refill its ring slot with the DMA of tile t + NPR, an
+    // n-block earlier than after the second n-block
+    if (par == 0 && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
   };
@@ -1410,10 +1426,12 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   // small batches (nq <= 128): the row-split kernel K1r, all queries in every wave
   // (VRQ_MFMA_ROWS=0: probe-build override)
   p->rows = nq <= kRowsMaxQueries && tuning_int("VRQ_MFMA_ROWS", 1) != 0;
+  int rows_occ = 1;  // K1r workgroups per CU of the chosen instance
   if (p->rows) {
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
     p->nqb = 1;
+    rows_occ = p->mb == 1 ? k1r_occ<1>() : p->mb == 2 ? k1r_occ<2>() : k1r_occ<4>();
   }
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
@@ -1432,7 +1450,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   // K1r with MB <= 2 runs the sample pass too (one sample chunk per wave); its MB = 4 instance would
   // spill in the dense epilogue, so batches of 65..128 queries take K1m's (MB = 2) sample pass
   p->rows_sample = p->rows && p->mb <= 2;
-  int64_t nsc = p->rows_sample ? 256 * MWAVES : 256 / p->nqb_s;
+  int64_t nsc = p->rows_sample ? 256 * MWAVES * rows_occ : 256 / p->nqb_s;
   // >= 8 chunks: >= 256 lane minima per query (>= 2K; very large batches would otherwise keep
   // fewer than K values and fall back to accepting every row)
   if (nsc < 8) nsc = 8;
@@ -1447,8 +1465,8 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->sample = tiles * RT;
   p->dvcols = nsc * 32;  // the dense pass writes 32 lane minima per (query, sample chunk)
   S = p->sample;
-  // thresholded pass over all n rows (K1r: one chunk per wave, 1024 waves)
-  int64_t want = p->rows ? 256 * MWAVES : 256 / p->nqb;
+  // thresholded pass over all n rows (K1r: one chunk per wave, 1024 waves per workgroup slot of a CU)
+  int64_t want = p->rows ? 256 * MWAVES * rows_occ : 256 / p->nqb;
   if (want < 1) want = 1;
   int64_t cr = (n + want - 1) / want;
   cr = (cr + RT - 1) / RT * RT;
