@@ -43,7 +43,7 @@
 
 // tools/build_g5_variants.sh compiles this file with VRQ_G5_BISECT bits set to time the matrix pass
 // with parts removed (1: threshold test, 2: LDS-DMA, 4: tile barrier, 8: MFMA, 16: candidate
-// flush; 2/4/8/16 give wrong results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
+// flush, 32: every other B-fragment read (each fragment feeds two k-steps' MFMAs); 2/4/8/16 give wrong results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
 // the library build.
 #ifndef VRQ_G5_BISECT
 #define VRQ_G5_BISECT 0
@@ -77,10 +77,12 @@ constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave <
 #define VRQ_G5_SEED 1
 #endif
 #ifndef VRQ_G5_HIT
-// thresholded pass, per-lane record of the tests of a tile: 2 = a hit bitmask built by the tests (the
+// thresholded pass, per-lane record of the tests of a tile: 3 = Phase III: one wave mask per test
+// (HWM below; Phase II keeps its integer seeds), 2 = a per-lane hit bitmask built by the tests (the
 // flush reads it: no recomputation); 1 = the running max only, the flush recomputes u - thr from the
-// still-live accumulators; 0 = a ures[] register file of the tests' values
-#define VRQ_G5_HIT 2
+// still-live accumulators; 0 = a ures[] register file of the tests' values.  Measured (10M x 1024,
+// nq = 1024, one box, two runs each): Phase-III main pass 8.74 / 8.64 ms (3) vs 8.82 / 8.92 (2)
+#define VRQ_G5_HIT 3
 #endif
 // timing-only probes of the DMA's cost (wrong results): 1 = every tile's DMA reads the chunk's first
 // tile (L2-resident source), 2 = the pieces are plain global loads into a discarded register (no LDS write)
@@ -99,6 +101,19 @@ constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave <
 #endif
 #ifndef VRQ_G5_REGSTAGE
 #define VRQ_G5_REGSTAGE 0
+#endif
+// thresholded pass with hit bitmasks (VRQ_G5_HIT == 2): the k-step of tile t at which tile t-2's hits
+// are flushed (the flush reads only the bitmask, no accumulator, so it can sit in the MFMA shadow);
+// -1 = before the tile's first B read, where it delays the tile's first MFMA
+// Phase-III passes: ring of 3 tiles with ONE barrier per tile at k-step 1 (tile t+1 landed and
+// visible, every wave done with tile t-1's slot, which tile t+2's DMA then refills), so the first B
+// fragments and the norm of tile t+1 are read during tile t's last k-steps: no barrier or LDS
+// latency between two tiles' MFMAs
+#ifndef VRQ_G5_XB
+#define VRQ_G5_XB 0
+#endif
+#ifndef VRQ_G5_FLUSH_STEP
+#define VRQ_G5_FLUSH_STEP 1
 #endif
 
 namespace vrq {
@@ -302,7 +317,8 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   // RS (register staging, Phase-III thresholded pass): ring of 2 images; during tile t each wave
   // writes its 8 staged rows of tile t+1 into the free image and loads its rows of tile t+2
   constexpr bool RS = P3 && !DENSE && VRQ_G5_REGSTAGE;
-  constexpr int NP = RS ? 2 : P3 ? (KShape<PH>::W8 ? VRQ_G5_NP3_W8 : VRQ_G5_NP3) : 4;
+  constexpr bool XB = P3 && !VRQ_G5_REGSTAGE && !VRQ_G5_NORM_REG && VRQ_G5_XB;
+  constexpr int NP = RS ? 2 : XB ? 3 : P3 ? (KShape<PH>::W8 ? VRQ_G5_NP3_W8 : VRQ_G5_NP3) : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
   constexpr int PPW = P3 ? RPW + 1 : 1;               // vector-memory instructions per wave per tile
@@ -468,6 +484,11 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   float th[KNE];
 #pragma unroll
   for (int e = 0; e < KNE; ++e) th[e] = DENSE ? 0.f : thr[qbase + qrow(e)];
+  // the thresholds land here, before the tile loop: the compiler's wait for a global load it still
+  // sees in flight would otherwise sit at their first use INSIDE the loop as an s_waitcnt vmcnt(0),
+  // which every tile then executes after issuing its LDS-DMA pieces (waiting for the next tile's DMA)
+#pragma unroll
+  for (int e = 0; e < KNE; ++e) asm volatile("" : "+v"(th[e]));
   constexpr bool SEED2 = !P3 && !DENSE && NPC == 1 && VRQ_G5_SEED;
   v16i seed[SEED2 ? 2 : 1];  // SEED2: -ceil(thr) of each accumulator register's query, clamped
   if constexpr (SEED2) {
@@ -495,11 +516,16 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   // UREC: the thresholded pass keeps only the running max; a flush recomputes u - thr from the
   // tile's accumulators, which stay live until the next-but-one tile's first MFMA.  HMASK: each test
   // shifts its hit bit into hm (test e -> bit KNE-1-e), the flush reads hm.  Both: no ures[] file.
-  constexpr bool HMASK = !DENSE && VRQ_G5_HIT == 2;
+  constexpr bool HMASK = !DENSE && VRQ_G5_HIT >= 2;
+  // HWM (VRQ_G5_HIT == 3): test e of a tile leaves its hits as one wave mask (v_cmp into an SGPR
+  // pair: cvt + fma + cmp per test, no per-lane bit assembly); the flush ORs the 16 masks on the
+  // scalar unit and builds per-lane bitmasks only for a tile with a hit
+  constexpr bool HWM = HMASK && P3 && VRQ_G5_HIT == 3;
   constexpr bool UREC = !DENSE && VRQ_G5_HIT >= 1;
   float ures[UREC ? 1 : KNE];
   float umax = -__builtin_inff(), uodd = 0.f;
   uint32_t hm = 0;
+  uint64_t hmk[HWM ? KNE : 1] = {};
 #pragma unroll
   for (int e = 0; e < (UREC ? 1 : KNE); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
   float invc = 0.f, invp = 0.f, invpp = 0.f;  // Phase III 1/||x|| of tiles t, t-1, t-2 (NaN: zero norm or past the chunk)
@@ -541,13 +567,29 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     const int lr = tstart(tt) + r;
     const bool ok = lane_valid(tt);
     if constexpr (!DENSE) {
-      if (!(VRQ_G5_BISECT & 16) && __ballot(SEED2 ? imax >= 0 : HMASK ? hm != 0 : umax >= 0.f)) {
+      bool fl;
+      if constexpr (HWM) {
+        uint64_t any = 0;
+#pragma unroll
+        for (int e = 0; e < KNE; ++e) any |= hmk[e];
+        fl = any != 0;
+      } else {
+        fl = __ballot(SEED2 ? imax >= 0 : HMASK ? hm != 0 : umax >= 0.f) != 0;
+      }
+      if (!(VRQ_G5_BISECT & 16) && fl) {
         uint32_t m = 0;  // (hits: ~k * n / sample rows per query over the corpus)
         if constexpr (SEED2) {
           static_for<0, KNE>([&](auto E) {
             constexpr int e = decltype(E)::value;
             m |= (((e >> 4) ? a1 : a0)[e & 15] >= 0 ? 1u : 0u) << (KNE - 1 - e);
           });
+        } else if constexpr (HWM) {
+#pragma unroll
+          for (int e = 0; e < KNE; ++e) {
+            uint32_t b;
+            asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b) : "v"(1u << (KNE - 1 - e)), "s"(hmk[e]));
+            m |= b;
+          }
         } else if constexpr (HMASK) {
           m = hm;
         } else {
@@ -597,6 +639,8 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   auto test = [&](float u, int e, bool vp) {
     if constexpr (DENSE) {
       ures[e] = fmaxf(ures[e], vp ? u : __builtin_nanf(""));
+    } else if constexpr (HWM) {
+      hmk[e] = __ballot(u >= 0.f);  // NaN: no hit
     } else if constexpr (HMASK) {
       hm = (hm << 1) | (u >= 0.f ? 1u : 0u);  // NaN: no hit
     } else if constexpr (UREC) {
@@ -622,6 +666,11 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   }
 
   int sl = 0;  // t % NP
+  constexpr int BA = VRQ_G5_BAHEAD;  // B fragments read BA k-steps ahead
+  constexpr int NR = BA < 4 ? 4 : 8; // ring (power of two > BA)
+  static_assert(!XB || (BA >= 1 && BA <= 8 && GKS % NR == 0), "cross-tile B ring");
+  v4i ringx[NR];                     // XB: the B ring and the norm carry over into the next tile
+  double nvx = 0.0;
   auto tile = [&](auto PAR, auto FIRST, int t) {
     constexpr int p = decltype(PAR)::value;
     constexpr bool first = decltype(FIRST)::value;  // tile 0: no previous tile to test
@@ -629,7 +678,15 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
     // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
     // the slots the DMA of this tile overwrites.
-    if constexpr (RS) {
+    if constexpr (XB) {
+      if constexpr (first) {  // tile 0 landed (tile 1's pieces may stay in flight)
+        if (ntiles > 1)
+          wait_vm<PPW>();
+        else
+          wait_vm<0>();
+        barrier_all();
+      }
+    } else if constexpr (RS) {
       // tile 0: its DMA and norm landed (tile 1's norm + 8 staged rows may stay in flight); later
       // tiles were written by this wave's ds_writes during the previous tile
       if (t == 0) {
@@ -647,14 +704,19 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
       else
         wait_vm<0>();
     }
-    if (!(VRQ_G5_BISECT & 4)) barrier_all();
-    if (!DENSE && t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);  // tile t-2's accumulators: acc[p] until this tile's first MFMA
+    if (!XB && !(VRQ_G5_BISECT & 4)) barrier_all();
+    // tile t-2's hits (its accumulators are acc[p] until this tile's first MFMA; the bitmask form
+    // needs none of them and flushes at k-step FLS instead)
+    constexpr int FLS = HMASK && !SEED2 ? VRQ_G5_FLUSH_STEP : -1;
+    if (FLS < 0 && !DENSE && t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);
     const bool vprev = DENSE ? lane_valid(t - 1) : true;  // (the sample pass's test of tile t-1)
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
     const bool dma = t + AHEAD < ntiles;
     const DmaTile dt = dma_tile(dma ? t + AHEAD : t, sl == 0 ? NP - 1 : sl - 1);
     const int sl1 = sl + 1 == NP ? 0 : sl + 1;                       // (t + 1) % NP
-    double nv = 0.0;
+    double nvl = 0.0;
+    double& nv = XB ? nvx : nvl;
+    const uint32_t slotn = sm0 + (uint32_t)(sl1 * PKT);  // XB: tile t+1's slot
     v4i pv = {};
     const uint32_t ubn = sm0 + (uint32_t)(NP * T2 + ((t + 1) & 1) * U2);  // Phase II: tile t+1 expanded here
     uint32_t badr[8];
@@ -664,23 +726,23 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
     } else if constexpr (P3) {
-      lds_read64(nv, slot + T3 + (uint32_t)(r * 8));
+      if (!XB || first) lds_read64(nv, slot + T3 + (uint32_t)(r * 8));  // (XB: read during tile t-1)
 #pragma unroll
       for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
     } else {
       badr[0] = sm0 + (uint32_t)(NP * T2 + (t & 1) * U2 + l * 16);
     }
-    constexpr int BA = VRQ_G5_BAHEAD;                 // B fragments read BA k-steps ahead
-    constexpr int NR = BA < 4 ? 4 : 8;                // ring (power of two > BA)
-    v4i ring[NR];
+    v4i ringl[NR];
+    v4i(&ring)[NR] = XB ? ringx : ringl;
     auto readB = [&](auto S) {
       constexpr int s = decltype(S)::value;
+      if constexpr ((VRQ_G5_BISECT & 32) && (s & 1)) return;  // probe: half the B reads
       if constexpr (P3)
         lds_read128_off<(s >> 3) * 256>(ring[s & (NR - 1)], badr[s & 7]);
       else
         lds_read128_off<s * 1024>(ring[s & (NR - 1)], badr[0]);
     };
-    static_for<0, BA>([&](auto S) { readB(S); });
+    if constexpr (!XB || first) static_for<0, BA>([&](auto S) { readB(S); });
     VRQ_SCHED_FENCE();
     static_for<0, GKS>([&](auto S) {
       constexpr int s = decltype(S)::value;
@@ -689,6 +751,12 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
         // everything but the BA newest LDS operations is complete: B(s), and the norm (issued
         // before B(0)) / the packed Phase-II tile (issued in step 1, before B(1 + BA))
         asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(ring[s & (NR - 1)]), "+v"(nv), "+v"(pv) : "n"(BA) : "memory");
+      } else if constexpr (XB) {
+        // tile t+1's norm and first B fragments (landed and visible since this tile's barrier)
+        constexpr int sn = s + BA - GKS;
+        if constexpr (sn == 0) lds_read64(nvx, slotn + T3 + (uint32_t)(r * 8));
+        lds_read128_off<(sn >> 3) * 256>(ring[(s + BA) & (NR - 1)], slotn + boff[sn & 7]);
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(BA) : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(GKS - 1 - s) : "memory");
       }
@@ -697,7 +765,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
           acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? seed[0] : acc[p][0]);
           acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? seed[SEED2 ? 1 : 0] : acc[p][1]);
         } else {
-          acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
+          acc[p][0] = mfma_i8(A[0][s], ring[((VRQ_G5_BISECT & 32) ? s & ~1 : s) & (NR - 1)], s == 0 ? zero : acc[p][0]);
           if constexpr (NA == 2) acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
         }
       } else if constexpr (s == 0) {
@@ -708,6 +776,17 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
         asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
       else
         asm volatile("" : "+v"(acc[p][0]));
+      if constexpr (XB && s == 1) {
+        // tile t+1 landed (its pieces were issued during tile t-1; none of tile t+2's yet) and is
+        // visible to every wave; every wave is done with tile t-1, whose slot tile t+2 refills
+        wait_vm<0>();
+        if (!(VRQ_G5_BISECT & 4)) barrier_all();
+        VRQ_SCHED_FENCE();
+      }
+      if constexpr (s == FLS && !DENSE) {
+        if (t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);
+        VRQ_SCHED_FENCE();
+      }
       // DMA of tile t + AHEAD, spread over the MFMA shadow
       if constexpr (RS) {
         // piece i at k-step 2 + DS*i: write staged row i of tile t+1 (loaded during tile t-1; the 8
@@ -759,6 +838,8 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
               asm volatile("" : "+v"(imax), "+v"(iodd));
             else if constexpr (DENSE)
               asm volatile("" : "+v"(ures[e]));
+            else if constexpr (HWM)
+              asm volatile("" : "+s"(hmk[e]));
             else if constexpr (HMASK)
               asm volatile("" : "+v"(hm));
             else if constexpr (UREC)
