@@ -46,6 +46,20 @@
 // folded by scalar carry-save ORs, and the hit's query row comes from its value's tag, not a mask;
 // 0 = always the 16-ballot walk.  Measured (profiles/r3_k1m_hit_tag_ab.txt): 1 beats 2 (c2 matrix
 // pass 0.39 vs 0.45 ms, c4 29.1 vs 29.6 ms), so 2 stays a probe-build option.
+// Thresholded passes: exact partial-distance pruning.  After k-steps 0..PK-1 (code bytes 0..8*PK-1)
+// the accumulator of (query q, row r) is A1 = tau'(q)/2 + <q, r>_1, and the rest of the dot is at
+// most pc_2(r), the popcount of the row's remaining bytes, so the row can still be a hit only if
+// A1 > (pc_1(r) - pc_2(r))/2 <= pc(r)/2.  An (M-block, n-block) pair where no lane's register
+// passes that bound skips its remaining MFMAs: its accumulators stay <= pc(r)/2 and the hit test
+// rejects them, so the candidates are exactly those of the full pass.  The row popcounts carry
+// pc_2 in their upper 16 bits.  0 = off.
+#ifndef VRQ_PRUNE
+#define VRQ_PRUNE 0
+#endif
+#ifndef VRQ_PRUNE_K
+#define VRQ_PRUNE_K 10  // even (a 16-byte piece boundary of the packed row)
+#endif
+static_assert(VRQ_PRUNE_K % 2 == 0 && VRQ_PRUNE_K > 0 && VRQ_PRUNE_K < 16, "prune k-step");
 #ifndef VRQ_HIT_FAST
 #define VRQ_HIT_FAST 1
 #endif
@@ -217,6 +231,8 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
+  constexpr bool PRUNE = !DENSE && VRQ_PRUNE;
+  constexpr int PK = VRQ_PRUNE_K;
   constexpr int QPW = MfmaShape<MB>::QPW, QPB = MfmaShape<MB>::QPB;
   __shared__ __attribute__((aligned(16))) uint8_t smem[MfmaShape<MB>::SMEM];
   uint8_t* pk = smem;                                       // NPK packed tiles
@@ -292,14 +308,16 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   }
   // row popcounts: tile rows 16w..16w+15, 4 lanes per row, 2 pieces each
   const int pr = 16 * w + (l >> 2), pc0 = 2 * (l & 3);
+  // PRUNE: weights of this lane's two pieces in the packed (pc | pc_2 << 16) row popcount
+  const int pwa = PRUNE && pc0 >= PK / 2 ? 65537 : 1, pwb = PRUNE && pc0 + 1 >= PK / 2 ? 65537 : 1;
   const uint32_t psrc0 = (uint32_t)(pk_slot(pr, pc0) * 16), psrc1 = (uint32_t)(pk_slot(pr, pc0 + 1) * 16);
   auto unpack_write = [&](const v2i& v, int u, uint32_t ubuf) __attribute__((always_inline)) {
     lds_write128(ubuf + udst[u], unpack_row32((uint32_t)v.x));
     lds_write128(ubuf + udst[u] + 1024, unpack_row32((uint32_t)v.y));
   };
   auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) __attribute__((always_inline)) {
-    int pc = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(c.x) + __popc(c.y) + __popc(c.z) +
-             __popc(c.w);
+    int pc = (__popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w)) * pwa +
+             (__popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w)) * pwb;
     pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
     pc += __builtin_amdgcn_update_dpp(0, pc, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
     if ((l & 3) == 0) lds_write32(pbuf + (uint32_t)(pr * 4), pc);
@@ -525,7 +543,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       }
     }
   };
-  auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) { return lr < nrows ? pcv : 0x40000000; };  // past the end: no hit
+  auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) {  // past the end: no hit
+    return lr < nrows ? (PRUNE ? pcv & 0xffff : pcv) : 0x40000000;
+  };
   // DENSE: the 16 values v = dist - pc(q) of block (m, n-block) (row lr of the chunk) fold into this
   // lane's running minima; only those leave the kernel (dense_out)
   DenseMin<DENSE, MB> dmin;
@@ -542,6 +562,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int m = 0; m < MB; ++m) hitm[m] = 0;
   int hpb = 0;   // the previous n-block's per-lane threshold pc(r)/2, as float bits
   v16f acc[2][MB];  // [n-block][m]
+  bool live[MB];     // PRUNE: (M-block, current n-block) may still hold a hit after k-step PK - 1
+#pragma unroll
+  for (int m = 0; m < MB; ++m) live[m] = true;
   if constexpr (!DENSE)
     static_for<0, MB>([&](auto M) {
       constexpr int m = decltype(M)::value;
@@ -656,7 +679,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
             asm volatile("" : "+v"(pc1));
           } else if constexpr (k == 2) {
-            pc0 += pc1;
+            pc0 = PRUNE ? pc0 * pwa + pc1 * pwb : pc0 + pc1;
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
             asm volatile("" : "+v"(pc0));
           } else {
@@ -709,11 +732,28 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           }
         }
       };
+      // PRUNE: this n-block's per-lane bound (pc_1 - pc_2)/2 (rows past the end: never live)
+      float hp1 = 0.f;
+      if constexpr (PRUNE && s == PK) {
+        const int v = pcv[nbk];
+        const int lr = t * RT + 32 * nbk + ri;
+        hp1 = lr < nrows ? 0.5f * (float)((v & 0xffff) - 2 * (v >> 16)) : 3.0e9f;
+      }
       static_for<0, MB>([&](auto M) {
         constexpr int m = decltype(M)::value;
         if constexpr (s == 0 && !DENSE)  // the seeds loaded after the block's last epilogue have landed
           asm volatile("" : "+v"(acc[nbk][m]));
-        if constexpr (!(VRQ_BISECT & 4))
+        if constexpr (PRUNE && s == PK) {  // any lane / register of (m, n-block) above its bound
+          const v16f& a = acc[nbk][m];
+          const float x0 = fmaxf(fmaxf(a[0], a[1]), a[2]), x1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
+          const float x2 = fmaxf(fmaxf(a[6], a[7]), a[8]), x3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
+          const float x4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
+          const float mx = fmaxf(fmaxf(fmaxf(x0, x1), x2), fmaxf(fmaxf(x3, x4), a[15]));
+          live[m] = __ballot(mx > hp1) != 0;
+        }
+        if constexpr (PRUNE && s >= PK && !(VRQ_BISECT & 4)) {
+          if (live[m]) acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], acc[nbk][m]);
+        } else if constexpr (!(VRQ_BISECT & 4))
           acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], (s == 0 && DENSE) ? v16f{} : acc[nbk][m]);
         else if constexpr (s == 0 && DENSE)
           acc[nbk][m] = v16f{};
