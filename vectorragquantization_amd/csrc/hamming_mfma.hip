@@ -59,6 +59,11 @@
 #ifndef VRQ_PRUNE_K
 #define VRQ_PRUNE_K 10  // even (a 16-byte piece boundary of the packed row)
 #endif
+// probe builds: 1 = the prune test and the per-MFMA branches run but never skip; 2 = the test runs,
+// every MFMA is issued (no branch)
+#ifndef VRQ_PRUNE_DIAG
+#define VRQ_PRUNE_DIAG 0
+#endif
 static_assert(VRQ_PRUNE_K % 2 == 0 && VRQ_PRUNE_K > 0 && VRQ_PRUNE_K < 16, "prune k-step");
 #ifndef VRQ_HIT_FAST
 #define VRQ_HIT_FAST 1
@@ -750,8 +755,16 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           const float x4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
           const float mx = fmaxf(fmaxf(fmaxf(x0, x1), x2), fmaxf(fmaxf(x3, x4), a[15]));
           live[m] = __ballot(mx > hp1) != 0;
+          if constexpr (VRQ_PRUNE_DIAG == 1) {
+            int one = 1;
+            asm volatile("" : "+s"(one));
+            live[m] = live[m] || one != 0;
+          } else if constexpr (VRQ_PRUNE_DIAG == 2) {
+            int lv = live[m];
+            asm volatile("" ::"s"(lv));
+          }
         }
-        if constexpr (PRUNE && s >= PK && !(VRQ_BISECT & 4)) {
+        if constexpr (PRUNE && s >= PK && VRQ_PRUNE_DIAG != 2 && !(VRQ_BISECT & 4)) {
           if (live[m]) acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], acc[nbk][m]);
         } else if constexpr (!(VRQ_BISECT & 4))
           acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], (s == 0 && DENSE) ? v16f{} : acc[nbk][m]);
