@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-recall", action="store_true")
     ap.add_argument("--no-encode", action="store_true", help="skip the encoder roofline leg")
+    ap.add_argument("--no-phase1", action="store_true",
+                    help="skip the config-3 Phase-I leg (roofline_phase1) of the default config-4 line")
     ap.add_argument("--scan", choices=["auto", "valu", "mfma"], default="auto",
                     help="Phase-I scan (auto = the library's choice for the shape)")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
@@ -162,7 +164,7 @@ class Pipeline:
 
     def step(self, record: bool):
         L, st = self.lib, N.stream_handle(self.codes.device)
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(7)] if record else None
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if record else None
         rec = (lambda i: e[i].record()) if record else (lambda i: None)
         rec(0)
         if self.kind == N.VRQ_SCAN_KIND_MFMA:
@@ -188,23 +190,27 @@ class Pipeline:
         if self.world > 1 and not self.phase1:
             nq = self.qf.shape[0]
             ids = self.rows  # external id = global row for the synthetic corpus
-            buf = gather_candidates(pack_candidates(self.cnt, self.rows, ids, self.dist, self.s2, self.s3))
+            local = pack_candidates(self.cnt, self.rows, ids, self.dist, self.s2, self.s3)
+            self.gather_bytes = int(local.numel())
+            buf = gather_candidates(local)
+            rec(7)
             gc, gr, gi, gd, g2, g3 = unpack_candidates(buf, self.world, nq, self.K)
             self.final = merge_shards(gc, gr, gd, g2, g3, self.k, self.K3)
         else:
             self.final = (self.cnt, self.rows, self.dist, self.s2, self.s3)
+            rec(7)
         rec(5)
         if record:
             self.ev.append(e)
 
     def stage_ms(self):
         """Mean ms per step of: scan (all stages), prefix stage, matrix stage, recheck stage, suffix stage,
-        finish (K2), all-gather + merge."""
+        finish (K2), all-gather + merge (and the all-gather alone)."""
         def mean(i, j):
             return float(np.mean([ev[i].elapsed_time(ev[j]) for ev in self.ev]))
         return {"scan": mean(0, 3), "prefix": mean(0, 1), "matrix": mean(1, 2), "recheck": mean(2, 6),
                 "suffix": mean(6, 3),
-                "finish": mean(3, 4), "collective": mean(4, 5)}
+                "finish": mean(3, 4), "collective": mean(4, 5), "allgather": mean(4, 7)}
 
 
 def recall_at_10(top_rows, qf, n_total, rank, world, dev, sample):
@@ -435,20 +441,48 @@ def pmc_traffic(tag, kernel):
         return None
 
 
+def _round_key(path):
+    """Sort key of a committed profile file name r<round>[s<session>]_...: (round, session)."""
+    import re
+    m = re.match(r"r(\d+)(?:s(\d+))?_", os.path.basename(path))
+    return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, 0)
+
+
 def rocprof_avg_ms(tag, kernel):
-    """Average duration (ms) of `kernel` in the newest committed rocprofv3 --kernel-trace --stats summary for
-    this workload tag (profiles/r*_<tag>_kernel_stats.csv), or None."""
+    """rocprofv3 duration (ms) of `kernel` for this workload tag from the newest committed summary:
+    profiles/r*_<tag>_dispatch.json (tools/trace_dispatches.py: the mean over the launches after the
+    bench's untimed warm-up steps, i.e. the launches the HIP events time) or else the --stats average of
+    profiles/r*_<tag>_kernel_stats.csv (every launch).  Returns (ms, source, what) or None."""
     import csv
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_kernel_stats.csv")))
-    if not files:
-        return None
+    disp = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_dispatch.json")), key=_round_key)
+    stats = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_kernel_stats.csv")), key=_round_key)
     try:
-        for row in csv.DictReader(open(files[-1])):
-            if kernel in row["Name"]:
-                return float(row["AverageNs"]) / 1e6, os.path.relpath(files[-1], HERE)
+        if disp and (not stats or _round_key(disp[-1]) >= _round_key(stats[-1])):
+            d = json.load(open(disp[-1]))
+            for name, v in d["kernels"].items():
+                if kernel in name:
+                    return (v["mean_after_warmup_ms"], os.path.relpath(disp[-1], HERE),
+                            f"rocprofv3 --kernel-trace: mean of the {v['n_after_warmup']} launches after "
+                            f"{d['warmup']} warm-up step(s), from the same bench command")
+        if stats:
+            for row in csv.DictReader(open(stats[-1])):
+                if kernel in row["Name"]:
+                    return (float(row["AverageNs"]) / 1e6, os.path.relpath(stats[-1], HERE),
+                            "rocprofv3 --kernel-trace --stats average over every launch (warm-up included)")
     except Exception:
         return None
     return None
+
+
+def rocprof_field(tag, kernel, work, unit_scale, peak, event_ms):
+    """The `rocprof` sub-object of a roofline: the committed profiler duration of the same kernel and
+    workload, its achieved rate and fraction, and the ratio of this run's HIP-event time to it."""
+    rp = rocprof_avg_ms(tag, kernel)
+    if not rp:
+        return None
+    ach = work / (rp[0] * 1e-3) / unit_scale
+    return {"avg_ms": rp[0], "achieved": ach, "frac": ach / peak, "source": rp[1], "what": rp[2],
+            "events_over_rocprof": event_ms / rp[0]}
 
 
 def measured_mfma_peak():
@@ -621,10 +655,8 @@ def run_c5(a, world, rank, dev):
             "mfma_issue_frac_i8": pieces * ops / (st["cosine_main"] * 1e-3) / 1e12 / I8_DENSE_PEAK_TOPS,
             "algorithmic_bytes_per_launch": m * 1024 + m * 8, "traffic": pmc_traffic(tag, "gemm_topk_kernel")}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    rp = rocprof_avg_ms(tag, "gemm_topk_kernel<3, false, false>")
-    if rp:  # the same kernel's rocprofv3 kernel-trace average (a profiled run of this workload)
-        roof["rocprof"] = {"avg_ms": rp[0], "achieved": ops / (rp[0] * 1e-3) / 1e12,
-                           "frac": ops / (rp[0] * 1e-3) / 1e12 / I8_DENSE_PEAK_TOPS, "source": rp[1]}
+    roof["rocprof"] = rocprof_field(tag, "gemm_topk_kernel<3, false, false>", ops, 1e12, I8_DENSE_PEAK_TOPS,
+                                    st["cosine_main"])
     roof_bin = {"achieved": ops / (st["binary_main"] * 1e-3) / 1e12, "kernel_ms": st["binary_main"],
                 "kernel": "gemm_topk_kernel<BINARY> main pass", "algorithmic_bytes_per_launch": m * 128}
     roof_bin["frac"] = roof_bin["achieved"] / roof["peak"]
@@ -648,6 +680,29 @@ def run_c5(a, world, rank, dev):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def visible_gpus(env=None, topology="/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process may use, counted WITHOUT initialising HIP (the launcher parent stays GPU-free):
+    the KFD topology's GPU nodes (simd_count > 0), narrowed by HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  Falls back to torch.cuda.device_count()
+    only where the topology is unreadable."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in os.listdir(topology):
+            with open(os.path.join(topology, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if line.strip())
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return torch.cuda.device_count()
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
 
 
 def launch_plan(gpus: int, env, device_count: int):
@@ -681,13 +736,16 @@ def launch_plan(gpus: int, env, device_count: int):
     return ("run", world, rank, local)
 
 
-def spawn_ranks(n: int) -> int:
+def spawn_ranks(n: int, build: bool = True) -> int:
     """Start n ranks of this script (same argv) as child processes with the torch.distributed env
     (127.0.0.1 rendezvous); rank 0's stdout is this process's stdout.  The parent never touches the
-    GPU.  If a rank fails, the others are terminated.  Returns the exit status."""
+    GPU (it counted the devices through the KFD topology, visible_gpus) and builds the library once before
+    the ranks start, so they never compile it concurrently.  If a rank fails, the others are terminated.  Returns the exit status."""
     import signal
     import socket
     import subprocess
+    if build:
+        N._build.build()  # (no GPU call: hipcc only, when the library is stale)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -718,22 +776,24 @@ def spawn_ranks(n: int) -> int:
 def main():
     a = parse()
     # --launch-probe (CPU tests of the launcher): pretend N devices, rendezvous over gloo, no GPU work
-    plan = launch_plan(a.gpus, os.environ, a.gpus if a.launch_probe else torch.cuda.device_count())
+    plan = launch_plan(a.gpus, os.environ, a.gpus if a.launch_probe else visible_gpus())
     if plan[0] == "refuse":
         log(f"bench.py: {plan[1]}")
         sys.exit(2)
     if plan[0] == "spawn":
-        sys.exit(spawn_ranks(plan[1]))
+        sys.exit(spawn_ranks(plan[1], build=not a.launch_probe))
     _, world, rank, local = plan
     if a.launch_probe:
+        rec = {"launch_probe": True, "n_gpus": world}
         if world > 1:
             dist.init_process_group("gloo", rank=rank, world_size=world)
             t = torch.tensor([rank], dtype=torch.int64)
             dist.all_reduce(t)
-            dist.destroy_process_group()
             assert int(t) == world * (world - 1) // 2
+            rec["multi_gpu"] = launch_probe_fields(world, rank)
+            dist.destroy_process_group()
         if rank == 0:
-            print(json.dumps({"launch_probe": True, "n_gpus": world}), flush=True)
+            print(json.dumps(rec), flush=True)
         return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -742,37 +802,269 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     if a.config == "c5":
         return run_c5(a, world, rank, dev)
+    if a.config == "c3":
+        return run_c3(a, world, rank, dev)
+    return run_3phase(a, world, rank, dev)
+
+
+PHASE1_NQS = (1, 8, 64)  # nq in {1, 8, 64} per pass
+
+
+def phase1_leg(dev, n, nqs, k, osb, steps, warmup, threads, cpu=True, scan="auto"):
+    """BASELINE config 3, the north star's numeric target: Phase-I-only Hamming top-K (K = k * osb)
+    over n uniform random 1024-bit codes (queries = corpus rows with 64-256 flipped
+    bits), at each batch size of `nqs` (the first nq queries of one query set).  Per batch size:
+    `warmup` untimed + `steps` timed passes, every stage bracketed by HIP events on the library's
+    stream; the dominant kernel (K1r, hamming_mfma_rows_kernel) is priced against HBM with its
+    algorithmic bytes n * 128 + nq * 128.  With `cpu`, the C restatement of FAISS hammings_knn_hc
+    (oracle/hamming_knn.c, checker) runs the largest query set over the same corpus on the host:
+    (dist, row) of the whole top-K and the top-10 ids must be identical at every nq."""
+    codes = synth.random_codes(n, device=dev)
+    qall, _ = synth.flip_queries(codes, max(nqs))
+    x8 = torch.empty((1, 1024), dtype=torch.int8, device=dev)
+    norms = torch.empty((1,), dtype=torch.float64, device=dev)
+    points, outs = {}, {}
+    for nq in nqs:
+        qb = qall[:nq].contiguous()
+        qf = torch.zeros((nq, 1024), dtype=torch.float32, device=dev)
+        P = Pipeline(codes, x8, norms, 0, n, qf, qb, k, osb, 1, 1, phase1_only=True, scan=scan)
+        for _ in range(warmup):
+            P.step(False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            P.step(True)
+        torch.cuda.synchronize()
+        T = time.perf_counter() - t0
+        st = P.stage_ms()
+        mb = n * 128 + nq * 128
+        kern = "hamming_mfma_rows_kernel<0" if P.kind == N.VRQ_SCAN_KIND_MFMA and nq <= 128 else \
+            ("hamming_mfma_kernel<0" if P.kind == N.VRQ_SCAN_KIND_MFMA else "hamming_scan_kernel")
+        kms = st["matrix"] if P.kind == N.VRQ_SCAN_KIND_MFMA else st["scan"]
+        ach = mb / (kms * 1e-3) / 1e9
+        pt = {"nq": nq, "qps": nq * steps / T, "ms_per_step": T / steps * 1e3, "phase_ms": st,
+              "kernel": kern.rstrip("<0"), "kernel_ms": kms, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+              "algorithmic_bytes_per_launch": mb, "timing": f"HIP events on the library's stream, {steps} passes "
+                                                            f"after {warmup} warm-up passes",
+              "mfma": {"achieved": 2048.0 * nq * n / (kms * 1e-3) / 1e12, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
+                       "frac": 2048.0 * nq * n / (kms * 1e-3) / 1e12 / MFMA_FP4_PEAK_TOPS}}
+        tag = f"c3_n{n}_nq{nq}_g1"
+        pt["rocprof"] = rocprof_field(tag, kern, mb, 1e9, HBM_PEAK_GBS, kms)
+        pt["traffic"] = pmc_traffic(tag, "hamming_mfma_rows_kernel")
+        points[str(nq)] = pt
+        outs[nq] = (P.dist.cpu().numpy(), P.rows.cpu().numpy())
+        del P
+    out = {"workload": f"BASELINE config 3: Phase-I-only Hamming top-{min(k * osb, n)} (k={k}), {n} x 1024 "
+                       "uniform random codes, queries = corpus rows with 64-256 flipped bits",
+           "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "peak_note": "8 TB/s spec; MI355X_MICROARCH.md measures 6.0-6.3 TB/s for plain in-order reads and "
+                        "6.5-6.8 TB/s chip-wide for non-temporal LDS-DMA streams (the load K1r uses)",
+           "target": "north_star: >= 0.50 of the HBM-read roofline at 100M rows, top-10 ids identical to the CPU",
+           "points": points}
+    if cpu:
+        lib = _oracle_lib()
+        codes_h = codes.cpu().numpy()
+        q_h = qall.cpu().numpy()
+        K = min(k * osb, n)
+        t0 = time.perf_counter()
+        D, I = cpu_phase1(lib, codes_h, q_h, K, threads)
+        t_all = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        cpu_phase1(lib, codes_h, q_h[:1], K, 1)
+        t_one = time.perf_counter() - t0
+        ident = {}
+        for nq, (gd, gr) in outs.items():
+            ident[str(nq)] = {"topK_dist_rows_identical": bool(np.array_equal(D[:nq], gd) and np.array_equal(I[:nq], gr)),
+                              "top10_ids_identical": float(np.mean([np.array_equal(a[:10], b[:10])
+                                                                    for a, b in zip(I[:nq], gr)]))}
+        out["cpu_gpu_identity"] = ident
+        out["identical_all"] = all(v["topK_dist_rows_identical"] for v in ident.values())
+        out["cpu_baseline"] = {"value": q_h.shape[0] / t_all, "unit": "queries/s", "kind": "port",
+                               **host_info(threads),
+                               "sample": f"{q_h.shape[0]} queries over the full {n}-row corpus in one call, C "
+                                         f"restatement of FAISS hammings_knn_hc (OpenMP over queries, {threads} "
+                                         f"threads, {t_all:.2f} s)",
+                               "single_core": {"value": 1.0 / t_one, "unit": "queries/s", "cores": 1,
+                                               "sample": "1 query (nq=1), 1 thread"}}
+        del codes_h
+    del codes, qall
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_c3(a, world, rank, dev):
+    """--config c3: the Phase-I-only line at one batch size (--nq, default 8) on one GPU."""
+    if world != 1:
+        log("bench.py: --config c3 is the single-GPU HBM-roofline configuration (BASELINE config 3)")
+        sys.exit(2)
+    n = a.n or CONFIGS["c3"]["n"]
+    nq = a.nq or CONFIGS["c3"]["nq"]
+    N.load()
+    t0 = time.perf_counter()
+    leg = phase1_leg(dev, n, (nq,), a.k, a.binary_oversample, a.steps, a.warmup, cpu_threads(a),
+                     cpu=not a.no_cpu_baseline, scan=a.scan)
+    pt = leg["points"][str(nq)]
+    log(f"[rank 0] c3 leg in {time.perf_counter() - t0:.1f} s")
+    roof = {k: pt[k] for k in ("achieved", "frac", "kernel", "kernel_ms", "algorithmic_bytes_per_launch", "timing",
+                               "mfma", "rocprof", "traffic")}
+    roof.update(bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s", rows=n)
+    out = {"metric": METRIC, "value": pt["qps"], "unit": "queries/s", "n_gpus": 1, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": pt["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic (uniform random 1024-bit codes, bit-flipped-row queries)",
+           "config": {"workload": f"{CONFIGS['c3']['name']}, {n} x 1024 corpus, nq={nq} queries per step",
+                      "corpus_rows": n, "nq": nq, "k": a.k, "binary_oversample": a.binary_oversample,
+                      "parallelism": "1 GPU"},
+           "phase_ms": pt["phase_ms"], "roofline": roof, "peak_note": leg["peak_note"]}
+    if "cpu_baseline" in leg:
+        out["cpu_baseline"] = leg["cpu_baseline"]
+        out["cpu_gpu_identity"] = leg["cpu_gpu_identity"][str(nq)]
+    print(json.dumps(out), flush=True)
+
+
+def cpu_shard_candidates(lib, codes_h, x8_of, row0, qf_h, qb_h, K, threads):
+    """One rank's part of the whole-corpus CPU restatement: its shard's exact top-K by (dist, row)
+    (hammings_knn_hc restatement) with global rows, and every candidate's Phase-II score (f64 dot with
+    2*unpackbits-1, CohereEnhancedVectorDB.py:283-293) and Phase-III score (f32 dot / f64 norm,
+    :302-318).  The union over shards holds the global top-K, so the merge below restates the
+    single-index search exactly."""
+    D, I = cpu_phase1(lib, codes_h, qb_h, K, threads)
+    res = []
+    for q in range(qb_h.shape[0]):
+        ok = I[q] >= 0
+        rows = I[q][ok]
+        pm = 2 * np.unpackbits(codes_h[rows], axis=1).astype(np.int32) - 1
+        s2 = pm.astype(np.float64) @ qf_h[q].astype(np.float64)
+        s3 = []
+        for r in rows:
+            v = x8_of(int(r))
+            nrm = np.linalg.norm(v)
+            s3.append(-np.inf if nrm == 0 else float(qf_h[q].dot(v)) / nrm)
+        res.append((D[q][ok], rows + row0, s2, np.array(s3, np.float64)))
+    return res
+
+
+def cpu_merge(parts, k, K, K3):
+    """Single-index semantics over the shards' candidates (CohereEnhancedVectorDB.py:267-322): global
+    top-K by (dist, row) -> stable sort by s2 desc -> first K3 -> stable sort by s3 desc -> first k."""
+    d = np.concatenate([p[0] for p in parts])
+    r = np.concatenate([p[1] for p in parts])
+    s2 = np.concatenate([p[2] for p in parts])
+    s3 = np.concatenate([p[3] for p in parts])
+    o = np.lexsort((r, d))[:K]
+    o2 = sorted(o.tolist(), key=lambda j: -s2[j])[:K3]
+    o3 = sorted(o2, key=lambda j: -s3[j])[:k]
+    return r[o3]
+
+
+def shard_sample_check(gpu_rows, K, K3, k, codes_h, x8_of, row0, qf_h, qb_h, threads, world, rank):
+    """Rank-0 check of the merged N-rank result on a query sample against the CPU restatement over the
+    WHOLE corpus: every rank restates its shard's part on its host (cpu_shard_candidates), rank 0
+    merges the parts (cpu_merge) and compares the final top-k rows with `gpu_rows` (rank 0's merged
+    GPU result for the sample, i64[nq, k], -1 padded).  Collective over the default group."""
+    lib = _oracle_lib()
+    t0 = time.perf_counter()
+    part = cpu_shard_candidates(lib, codes_h, x8_of, row0, qf_h, qb_h, K, threads)
+    parts = [None] * world
+    if world > 1:
+        dist.all_gather_object(parts, part)
+    else:
+        parts = [part]
+    if rank != 0:
+        return None
+    same = []
+    for q in range(qf_h.shape[0]):
+        ref = cpu_merge([p[q] for p in parts], k, K, K3)
+        g = gpu_rows[q][gpu_rows[q] >= 0]
+        same.append(bool(np.array_equal(ref, g)))
+    return {"queries": int(qf_h.shape[0]), "top10_identical": float(np.mean(same)),
+            "seconds": time.perf_counter() - t0,
+            "checker": "C hammings_knn_hc restatement + NumPy Phases II/III over each rank's shard on its host, "
+                       "merged on rank 0 with the single-index rule (test infrastructure)"}
+
+
+def multi_gpu_fields(st, gather_bytes, dev):
+    """The N > 1 line's view of the run from the process group: its size and backend, per-rank min / max
+    of the stage times (shard imbalance) and the exchange (bytes, time).  Collective over the default
+    group; every rank returns the same dict."""
+    world = dist.get_world_size()
+    mine = torch.tensor([st["matrix"], st["scan"], st["finish"], st["allgather"], st["collective"]],
+                        dtype=torch.float64, device=dev)
+    allr = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    allr = torch.stack(allr).cpu().numpy()
+    return {"world_size_process_group": world, "backend": dist.get_backend(),
+            "rank_matrix_ms": {"min": float(allr[:, 0].min()), "max": float(allr[:, 0].max())},
+            "rank_scan_ms": {"min": float(allr[:, 1].min()), "max": float(allr[:, 1].max())},
+            "rank_finish_ms": {"min": float(allr[:, 2].min()), "max": float(allr[:, 2].max())},
+            "allgather": {"bytes_per_rank": gather_bytes, "bytes_total": gather_bytes * world,
+                          "ms_max_over_ranks": float(allr[:, 3].max()),
+                          "with_merge_ms_max_over_ranks": float(allr[:, 4].max()),
+                          "collective": "one all_gather_into_tensor (RCCL over xGMI) + vrq_merge_shards"}}
+
+
+def launch_probe_fields(world, rank):
+    """--launch-probe (CPU, gloo): the N > 1 line's fields on synthetic stage times, and the sample check
+    on a small corpus sharded like bench.py's, with rank 0's "GPU" rows taken from the single-index
+    oracle over the whole corpus (oracle_np.three_phase_batch)."""
+    from oracle import oracle_np as O
+    st = {"matrix": 1.0 + rank, "scan": 2.0 + rank, "finish": 0.1, "allgather": 0.05 * (rank + 1),
+          "collective": 0.2}
+    fields = multi_gpu_fields(st, 1234, torch.device("cpu"))
+    rng = np.random.default_rng(11)
+    n, nq, k, osb, osi = 6400, 8, 10, 10, 3
+    codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    codes[3000:3200] = codes[5]                               # ties across the shard boundary
+    x8 = rng.integers(-127, 128, (n, 1024), dtype=np.int8)
+    qf = rng.standard_normal((nq, 1024)).astype(np.float32)
+    qb = codes[rng.integers(0, n, nq)] ^ rng.integers(0, 2, (nq, 128), dtype=np.uint8)
+    r0, r1 = synth.shard_range(n, rank, world)
+    gpu = None
+    if rank == 0:
+        ref = O.three_phase_batch(codes, x8, np.arange(n), qf, qb, k, osb, osi)
+        gpu = np.full((nq, k), -1, np.int64)
+        for q in range(nq):
+            gpu[q, :ref[q]["row"].shape[0]] = ref[q]["row"]
+    fields["sample_check"] = shard_sample_check(gpu, k * osb, k * osi, k, np.ascontiguousarray(codes[r0:r1]),
+                                                lambda r: x8[r0 + r], r0, qf, qb, 2, world, rank)
+    return fields
+
+
+def run_3phase(a, world, rank, dev):
+    """Configs 4 (default) and 2: the three-phase search of an nq-query batch, row-sharded over the ranks."""
     cfg = CONFIGS[a.config]
-    phase1 = cfg["phase1"]
     n = a.n or cfg["n"]
     nq = a.nq or cfg["nq"]
     N.load()
     t_setup = time.perf_counter()
-    if phase1:
-        r0, r1 = synth.shard_range(n, rank, world)
-        codes = synth.random_codes(r1 - r0, device=dev, seed=synth.SEED + 77 * rank)
-        x8 = torch.empty((1, 1024), dtype=torch.int8, device=dev)
-        norms = torch.empty((1,), dtype=torch.float64, device=dev)
-        qb, _ = synth.flip_queries(codes, nq)
-        if world > 1:
-            dist.broadcast(qb, 0)
-        qf = torch.zeros((nq, 1024), dtype=torch.float32, device=dev)
-        row0 = r0
-    else:
-        shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
-        codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
-        qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+    codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
+    qf, qb, _ = synth.make_queries(n, nq, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
 
-    P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, phase1,
+    P = Pipeline(codes, x8, norms, row0, n, qf, qb, a.k, a.binary_oversample, a.int8_oversample, world, False,
                  a.scan)
     T = timed_loop(P, a, world, dev)
+    st = P.stage_ms()
 
     top_rows = P.final[1]
     rec = None
-    if not a.no_recall and not phase1:
+    if not a.no_recall:
         rec = recall_at_10(top_rows, qf, n, rank, world, dev, min(a.recall_sample, nq))
+    multi = None
+    if world > 1:
+        multi = multi_gpu_fields(st, P.gather_bytes, dev)
+        if not a.no_cpu_baseline:
+            ns = min(16, nq)
+            cache = {}
+
+            def x8_of(r):
+                if r not in cache:
+                    cache[r] = x8[r].cpu().numpy()
+                return cache[r]
+            multi["sample_check"] = shard_sample_check(
+                P.final[1][:ns].cpu().numpy(), P.K, P.K3, a.k, codes.cpu().numpy(), x8_of, row0,
+                qf[:ns].cpu().numpy(), qb[:ns].cpu().numpy(), cpu_threads(a), world, rank)
 
     if rank != 0:
         if world > 1:
@@ -782,47 +1074,32 @@ def main():
 
     m = codes.shape[0]
     K = P.K
-    st = P.stage_ms()
     tag = f"{a.config}_n{n}_nq{nq}_g{world}"
     # whole Phase-I scan against HBM: algorithmic bytes = corpus codes + queries + K keys/query
     scan_bytes = m * 128 + nq * 128 + nq * K * 12
     roof_scan_hbm = {"bound": "hbm", "achieved": scan_bytes / (st["scan"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": scan_bytes / (st["scan"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "scope": "all Phase-I stages", "ms": st["scan"], "algorithmic_bytes": scan_bytes}
+    roof_valu = None
     if P.kind == N.VRQ_SCAN_KIND_MFMA:
         # dominant kernel: hamming_mfma_kernel over rows [prefix, m): one 1024-bit AND-popcount
         # = 1024 MACs = 2048 ops per (query, row), real queries only (padding not counted)
         rows_m = m - P.prefix_rows
         ops = 2048.0 * nq * rows_m
         ach = ops / (st["matrix"] * 1e-3) / 1e12
+        kern = "hamming_mfma_rows_kernel<0" if nq <= 128 else "hamming_mfma_kernel<0"
         roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
-                "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, "hamming_mfma_kernel"),
-                "kernel": "hamming_mfma_kernel (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
-                "kernel_ms": st["matrix"], "algorithmic_ops_per_launch": ops,
-                "algorithmic_bytes_per_launch": rows_m * 128 + nq * 128,
+                "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, kern.rstrip("<0")),
+                "kernel": f"{kern.rstrip('<0')} (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
+                "kernel_ms": st["matrix"], "timing": "HIP events on the library's stream, this run",
+                "algorithmic_ops_per_launch": ops, "algorithmic_bytes_per_launch": rows_m * 128 + nq * 128,
                 "measured_sustained_peak": measured_mfma_peak(), "rows": rows_m,
                 "prefix_rows_exact_scan": P.prefix_rows}
-        rp = rocprof_avg_ms(tag, "hamming_mfma_kernel<0")
-        if rp:  # the same kernel's rocprofv3 kernel-trace average (a profiled run of this workload)
-            roof["rocprof"] = {"avg_ms": rp[0], "achieved": ops / (rp[0] * 1e-3) / 1e12,
-                               "frac": ops / (rp[0] * 1e-3) / 1e12 / MFMA_FP4_PEAK_TOPS, "source": rp[1]}
-        roof_valu = None
-        if phase1:
-            # config 3 (Phase I only, few queries) is priced against HBM (north_star: >= 50 % of the
-            # HBM-read roofline at 100M): the matrix kernel's algorithmic bytes / its time
+        roof["rocprof"] = rocprof_field(tag, kern, ops, 1e12, MFMA_FP4_PEAK_TOPS, st["matrix"])
+        if nq <= 128:  # small batches (config-2 latency leg): K1r streams the codes, priced against HBM too
             mb = rows_m * 128 + nq * 128
-            roof = {"bound": "hbm", "achieved": mb / (st["matrix"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": mb / (st["matrix"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "traffic": pmc_traffic(tag, "hamming_mfma_rows_kernel"),
-                    "kernel": "hamming_mfma_rows_kernel (row-split FP4 MFMA scan, small batches)",
-                    "kernel_ms": st["matrix"], "timing": "HIP events on the library's stream, this run",
-                    "algorithmic_bytes_per_launch": mb, "rows": rows_m,
-                    "mfma": {"achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
-                             "frac": ach / MFMA_FP4_PEAK_TOPS}}
-            rp = rocprof_avg_ms(tag, "hamming_mfma_rows_kernel<0")
-            if rp:  # the same kernel's rocprofv3 kernel-trace average (a profiled run of this workload)
-                roof["rocprof"] = {"avg_ms": rp[0], "achieved": mb / (rp[0] * 1e-3) / 1e9,
-                                   "frac": mb / (rp[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, "source": rp[1]}
+            roof["hbm"] = {"achieved": mb / (st["matrix"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": mb / (st["matrix"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
     else:
         roof = dict(roof_scan_hbm, traffic=pmc_traffic(tag, "hamming_scan_kernel"),
                     kernel="hamming_scan_kernel (wavefront popcount)", kernel_ms=st["scan"])
@@ -832,9 +1109,8 @@ def main():
     out = {
         "metric": METRIC, "value": nq * a.steps / T, "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "u8" if phase1 else "u8+f64",
-        "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)"
-                if not phase1 else "synthetic (uniform random 1024-bit codes, bit-flipped-row queries)",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8+f64",
+        "data": "synthetic (SURVEY.md 8(d) clustered d=1024 generator; int8/ubinary from the gfx950 encoder)",
         "config": {"workload": f"{cfg['name']}, {n} x 1024 corpus, nq={nq} queries per step",
                    "corpus_rows": n, "rows_per_gpu": m, "nq": nq, "k": a.k, "binary_oversample": a.binary_oversample,
                    "int8_oversample": a.int8_oversample, "parallelism": f"row-shard x{world} + RCCL all_gather"
@@ -843,15 +1119,19 @@ def main():
         "phase_ms": st, "scan_kind": "mfma" if P.kind == N.VRQ_SCAN_KIND_MFMA else "valu",
         "roofline": roof, "roofline_scan_hbm": roof_scan_hbm, "roofline_valu": roof_valu,
     }
-    if not phase1 and not a.no_recall:
+    if multi:
+        out["multi_gpu"] = multi
+    if not a.no_recall:
         out["recall_note"] = ("recall_at_10 is vs exact float32 IP over the synthetic generator's floats; its "
                               "top-10 beyond the query's source row is a near-tie among ~n/4096 cluster-mates, which "
                               "sign-bit codes cannot resolve (the CPU path agrees exactly). real_data is the same "
                               "GPU search on the reference's own persisted Cohere corpus.")
         out["real_data"] = real_data_recall(dev)
     threads = cpu_threads(a)
-    if world == 1 and not a.no_cpu_baseline and not phase1:
-        sample = a.cpu_sample or (1024 if n <= 2_000_000 else 64)
+    if world == 1 and nq <= 16:
+        out["latency"] = search_latency(codes, x8, norms, qf, qb, a, dev)
+    if world == 1 and not a.no_cpu_baseline:
+        sample = a.cpu_sample or min(nq, 1024 if n <= 2_000_000 else 64)
         x8_src = x8
 
         def fetch_x8(rows):
@@ -866,17 +1146,42 @@ def main():
         out["cpu_baseline"] = cb
         out["cpu_gpu_top10_identical"] = parity
         del codes_h
-    elif world == 1 and not a.no_cpu_baseline and phase1:
-        cb, ident = cpu_baseline_phase1(codes.cpu().numpy(), qb.cpu().numpy(), K, threads,
-                                        P.dist.cpu().numpy(), P.rows.cpu().numpy())
-        out["cpu_baseline"] = cb
-        out["cpu_gpu_identity"] = ident
-    if world == 1 and not phase1 and not a.no_encode:
+    if world == 1 and not a.no_encode:
         out["roofline_encode"] = encode_roofline(dev)
+    if world == 1 and a.config == "c4" and not a.no_phase1:
+        # the north star's target (BASELINE config 3) measured in the same run: the config-4 corpus
+        # stays resident (117 GB) beside the 12.8 GB Phase-I corpus
+        t0 = time.perf_counter()
+        out["roofline_phase1"] = phase1_leg(dev, CONFIGS["c3"]["n"], PHASE1_NQS, a.k, a.binary_oversample,
+                                            a.steps, a.warmup, threads, cpu=not a.no_cpu_baseline)
+        log(f"[rank 0] Phase-I leg in {time.perf_counter() - t0:.1f} s")
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def search_latency(codes, x8, norms, qf, qb, a, dev, calls=200):
+    """Single-query latency through the Python drop-in surface (SURVEY.md 8(d) config 2's nq=1 leg; the
+    reference's search() answers one query per call, CohereEnhancedVectorDB.py:227-322): host wall time
+    of search3 on one host-resident query -- H2D of the f32 + ubinary query, the scan stages, the
+    finish, D2H of the top-k -- median and p99 over `calls` calls after 10 warm-up calls."""
+    from vectorragquantization_amd.enhanced import search3
+    qf_h = qf[:1].cpu().pin_memory()
+    qb_h = qb[:1].cpu().pin_memory()
+    ts = []
+    for i in range(calls + 10):
+        t0 = time.perf_counter()
+        c, r, d, s2, s3 = search3(codes, x8, norms, qf_h.to(dev, non_blocking=True), qb_h.to(dev, non_blocking=True),
+                                  a.k, a.binary_oversample, a.int8_oversample)
+        r.cpu()
+        if i >= 10:
+            ts.append(time.perf_counter() - t0)
+    ts = np.array(ts) * 1e3
+    return {"queries_per_call": 1, "calls": calls, "median_ms": float(np.median(ts)),
+            "p99_ms": float(np.percentile(ts, 99)), "min_ms": float(ts.min()),
+            "what": "host wall time of one enhanced.search3 call (H2D query, Phase I-III on the GPU, D2H top-k), "
+                    "workspace allocated per call by the caching allocator"}
 
 
 if __name__ == "__main__":

@@ -60,7 +60,10 @@ extern "C" {
 #define VRQ_SCAN_STAGE_SUFFIX 64 /* candidates -> one sorted K-list per query (exact rescan on
                                     list overflow) */
 
-/* encoder modes for vrq_encode */
+/* encoder modes for vrq_encode.  Inputs must be finite: the reference's NumPy encoders give NaN
+ * min/max, NaN means and platform-defined integer casts for a NaN element, so no NaN behaviour is
+ * pinned; the d = 1024 kernels fold min/max with v_med3 (a NaN element yields min = -inf, i.e. an
+ * all-zero local code) and the generic kernel with fminf/fmaxf (NaN elements ignored). */
 #define VRQ_ENC_INT8_GLOBAL 0  /* VectorDBInt8Global._quantize_to_int8 + _to_binary */
 #define VRQ_ENC_INT16_GLOBAL 1 /* VectorDBInt16Global._quantize_to_int16 + _to_binary */
 #define VRQ_ENC_INT4_GLOBAL 2  /* VectorDBInt4Global._quantize_to_int4 (limit ignored) + _to_binary */
@@ -237,6 +240,11 @@ size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t dim, int32_
 /* int8 pieces per query of this build's matrix pass (1: q ~ S*a, 2: q ~ S*(a + b/256)); the
  * algorithmic ops of a pass are 2*nq*n*dim either way (for roofline reporting) */
 int vrq_gemm_topk_pieces(void);
+/* Host-only planning introspection (no reference counterpart; for tests and tools): the matrix
+ * passes' plan of a vrq_gemm_topk / vrq_flat_ip_topk call shape.  info i64[8] = chunk rows, chunks,
+ * per-(query, chunk) list capacity, query blocks, sample chunks, rows per sample chunk, workspace
+ * bytes, queries per block.  VRQ_EUNSUPPORTED for shapes the path does not serve. */
+int vrq_gemm_topk_plan(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k, int64_t* info);
 int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
                   int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
                   int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,

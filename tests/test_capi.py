@@ -121,3 +121,22 @@ def test_release_library_ignores_tuning_environment(monkeypatch):
     assert lib.vrq_gemm_topk_workspace_size(*args) == base
     assert lib.vrq_search3_workspace_size(1_000_000, 1024, 1024, 100) == s3
     assert probe.vrq_gemm_topk_workspace_size(*args) != base
+
+
+def test_gemm_plan_chunk_rows_fit_the_hit_stage():
+    """the thresholded pass stages a hit as (query-in-wave << 26 | chunk row), so
+    every plan keeps chunk rows below 2^26 -- at large n with few chunks per query block (large nq)
+    too -- and the workspace size equals the planned one."""
+    import numpy as np
+    lib = N.load()
+    info = np.zeros(8, np.int64)
+    for mode in (2, 3, 4):
+        for n in (1000, 10_000_000, 300_000_000, (1 << 32) - 1):
+            for nq in (1, 1024, 65536):
+                assert lib.vrq_gemm_topk_plan(mode, n, 1024, nq, 10, info.ctypes.data) == N.VRQ_OK
+                chunk_rows, nchunks = int(info[0]), int(info[1])
+                assert 0 < chunk_rows < (1 << 26) and chunk_rows % 32 == 0
+                assert nchunks == -(-n // chunk_rows) and nchunks <= 2048
+                assert info[6] == lib.vrq_gemm_topk_workspace_size(mode, n, 1024, nq, 10)
+    assert lib.vrq_gemm_topk_plan(3, 1 << 32, 1024, 1, 10, info.ctypes.data) == N.VRQ_EUNSUPPORTED
+    assert lib.vrq_gemm_topk_plan(1, 1000, 1024, 1, 10, info.ctypes.data) == N.VRQ_EUNSUPPORTED

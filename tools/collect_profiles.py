@@ -3,6 +3,7 @@
 committed profiles/ directory under the names bench.py looks up:
   profiles/<round>_<config>_n<rows>_nq<nq>_g1_kernel_stats.csv   (kernel-trace --stats summary)
   profiles/<round>_<config>_n<rows>_nq<nq>_g1_pmc.json           (tools/summarize_profile.py summary)
+  profiles/<round>_<config>_n<rows>_nq<nq>_g1_dispatch.json      (tools/trace_dispatches.py summary)
 Usage: collect_profiles.py <round, e.g. r3> <gpurun_out/TAG> [--n config=rows ...]"""
 import glob
 import os
@@ -22,6 +23,9 @@ def main(rnd, src, overrides):
             glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
         if stats:
             shutil.copy(stats[0], os.path.join(here, "profiles", f"{tag}_kernel_stats.csv"))
+        disp = os.path.join(d, "dispatch.json")
+        if os.path.exists(disp):
+            shutil.copy(disp, os.path.join(here, "profiles", f"{tag}_dispatch.json"))
         summ = os.path.join(d, "summary.json")
         if os.path.exists(summ):
             shutil.copy(summ, os.path.join(here, "profiles", f"{tag}_pmc.json"))

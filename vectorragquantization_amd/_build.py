@@ -48,17 +48,29 @@ def up_to_date(lib: str = LIB) -> bool:
     return all(os.path.getmtime(d) <= t for d in _deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Build libvrq.so and libvrq_probe.so (whichever is stale); returns the release library path."""
-    todo = [(lib, probe) for lib, probe in ((LIB, False), (PROBE_LIB, True)) if force or not up_to_date(lib)]
-    if not todo:
-        return LIB
-    hipcc = _hipcc()
+class _BuildLock:
+    """Exclusive lock on the object directory: concurrent loaders (the ranks of one job, the two
+    workers of a test) build one after another, and the later ones find the library up to date."""
 
-    def compile_one(job):
-        src, probe = job
-        odir = os.path.join(OBJDIR, "probe") if probe else OBJDIR
-        os.makedirs(odir, exist_ok=True)
+    def __enter__(self):
+        import fcntl
+        os.makedirs(OBJDIR, exist_ok=True)
+        self.f = open(os.path.join(OBJDIR, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
+def _build_one(lib: str, probe: bool, verbose: bool) -> None:
+    hipcc = _hipcc()
+    odir = os.path.join(OBJDIR, "probe") if probe else OBJDIR
+    os.makedirs(odir, exist_ok=True)
+
+    def compile_one(src):
         obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc, *CFLAGS, *(["-DVRQ_TUNING_ENV"] if probe else []), *EXTRA.get(src, []), "-c",
                os.path.join(CSRC, src), "-o", obj]
@@ -69,18 +81,34 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(r.stderr, file=sys.stderr)
         return obj
 
-    jobs = [(src, probe) for _, probe in todo for src in SOURCES]
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
-        objs = list(ex.map(compile_one, jobs))
-    for i, (lib, _) in enumerate(todo):
-        tmp = lib + ".tmp"
-        r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC",
-                            *objs[i * len(SOURCES):(i + 1) * len(SOURCES)], "-o", tmp], capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link of {os.path.basename(lib)} failed:\n{r.stderr}")
-        os.replace(tmp, lib)
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = lib + ".tmp"
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link of {os.path.basename(lib)} failed:\n{r.stderr}")
+    os.replace(tmp, lib)
+
+
+def build(force: bool = False, verbose: bool = False, probe: bool = False) -> str:
+    """Build libvrq.so (or, with ``probe``, libvrq_probe.so) if stale; returns its path.  The release
+    library never depends on the probe build."""
+    lib = PROBE_LIB if probe else LIB
+    if not force and up_to_date(lib):
+        return lib
+    with _BuildLock():
+        if force or not up_to_date(lib):  # (another process may have built it while we waited)
+            _build_one(lib, probe, verbose)
+    return lib
+
+
+def build_all(force: bool = False, verbose: bool = False) -> str:
+    """The release library first, then the probe build (tools/ sweeps and two tests load it)."""
+    build(force, verbose)
+    build(force, verbose, probe=True)
     return LIB
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build_all(force="--force" in sys.argv, verbose=True))

@@ -70,6 +70,7 @@ SIGNATURES = {
     "vrq_rescore_dequant": (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _D, _I64, _P, _I32, _P, _P]),
     "vrq_gemm_topk_workspace_size": (_SZ, [_I32, _I64, _I32, _I32, _I32]),
     "vrq_gemm_topk_pieces": (C.c_int, []),
+    "vrq_gemm_topk_plan": (C.c_int, [_I32, _I64, _I32, _I32, _I32, _P]),
     "vrq_gemm_topk": (C.c_int, [_I32, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,
                                 _P]),
     "vrq_flat_ip_prepare": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),
@@ -86,14 +87,26 @@ _lib = None
 _lock = threading.Lock()
 
 
+_override = None
+
+
+def use_library(path: str) -> None:
+    """Load ``path`` instead of the in-tree libvrq.so in this process (tools/ sweeps of probe variants
+    and tests only; call before the first load()).  The product never reads the environment for it."""
+    global _override, _lib
+    if _lib is not None:
+        raise VrqNativeError("use_library() after the library was loaded")
+    _override = path
+
+
 def lib_path() -> str:
-    return os.environ.get("VRQ_LIB", _build.LIB)
+    return _override or _build.LIB
 
 
-def _open(path: str, default: str):
+def _open(path: str, default: str, probe: bool = False):
     if not os.path.exists(path) or (path == default and not _build.up_to_date(default)):
         try:
-            _build.build()
+            _build.build(probe=probe)
         except Exception as e:  # no hipcc on this host and no prebuilt library
             if not os.path.exists(path):
                 raise VrqNativeError(f"{os.path.basename(path)} missing and cannot be built: {e}") from e
@@ -131,7 +144,7 @@ def load_probe():
     global _probe
     with _lock:
         if _probe is None:
-            _probe = _open(_build.PROBE_LIB, _build.PROBE_LIB)
+            _probe = _open(_build.PROBE_LIB, _build.PROBE_LIB, probe=True)
         return _probe
 
 

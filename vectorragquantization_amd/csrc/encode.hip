@@ -447,7 +447,10 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
     float scale = gscale;
     bool flat = false;
     if constexpr (MODE == VRQ_ENC_INT4_GLOBAL || MODE == VRQ_ENC_INT8_LOCAL || MODE == VRQ_ENC_INT4_LOCAL) {
-      // min / max as v_med3 against -+inf (no NaN canonicalisation per element)
+      // min / max as v_med3 against -+inf (no NaN canonicalisation per element).  Inputs must be
+      // finite (include/vrq.h): a NaN element makes v_med3 return the min3 of its operands, so
+      // mn = -inf and the local code is all zero; the generic kernel's fminf/fmaxf ignore NaNs.  The
+      // reference has no defined NaN result to match (NumPy min/max/mean propagate NaN into the cast).
       float mn = e[0], mx = e[0];
 #pragma unroll
       for (int i = 1; i < 16; ++i) {

@@ -70,6 +70,7 @@
 #define VRQ_G5_STAGE 1
 #endif
 constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave << 26 | chunk row)
+constexpr int64_t kMaxChunkRows = (int64_t(1) << 26) - 32;  // chunk rows fit the stage's 26-bit field
 #ifndef VRQ_G5_SEED
 // Phase-II thresholded pass: the accumulators start at -ceil(thr) (an integer seed per query: the
 // binary u is the integer dot), so a test is one integer max per accumulator register and the flush
@@ -1351,6 +1352,9 @@ static int gemm_plan(int64_t n, int nq, int k, GemmPlan* p) {
   int64_t cr = (n + want - 1) / want;
   cr = (cr + GRT - 1) / GRT * GRT;
   if ((n + cr - 1) / cr > MAX_CHUNKS) cr = ((n + MAX_CHUNKS - 1) / MAX_CHUNKS + GRT - 1) / GRT * GRT;
+  // the thresholded pass's hit stage packs (query-in-wave << 26 | chunk row): chunks stay below 2^26
+  // rows (n < 2^32 then needs at most 65 chunks, far below MAX_CHUNKS)
+  if (cr > kMaxChunkRows) cr = kMaxChunkRows;
   p->chunk_rows = cr;
   p->nchunks = (int)((n + cr - 1) / cr);
   const int64_t Sv = S < n ? S : n;
@@ -1549,6 +1553,23 @@ extern "C" size_t vrq_gemm_topk_workspace_size(int32_t mode, int64_t n, int32_t 
   GemmPlan p;
   if (!gemm_mode_ok(mode) || dim != DIM || gemm_plan(n, nq, k, &p) != VRQ_OK) return 0;
   return p.bytes;
+}
+
+extern "C" int vrq_gemm_topk_plan(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k, int64_t* info) {
+  GemmPlan p;
+  if (!info) return VRQ_EINVAL;
+  if (!gemm_mode_ok(mode) || dim != DIM) return VRQ_EUNSUPPORTED;
+  const int rc = gemm_plan(n, nq, k, &p);
+  if (rc != VRQ_OK) return rc;
+  info[0] = p.chunk_rows;
+  info[1] = p.nchunks;
+  info[2] = p.capc;
+  info[3] = p.nqb;
+  info[4] = p.nsc;
+  info[5] = p.scr;
+  info[6] = (int64_t)p.bytes;
+  info[7] = GQB;
+  return VRQ_OK;
 }
 
 extern "C" int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,

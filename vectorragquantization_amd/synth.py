@@ -48,7 +48,8 @@ def shard_range(n_total: int, rank: int, world: int, grid_chunks: int = 64):
     cs = chunk_grid(n_total, grid_chunks)
     per = grid_chunks // world
     r0 = min(n_total, rank * per * cs)
-    r1 = min(n_total, (rank + 1) * per * cs)
+    # the last rank takes the grid's remainder when world does not divide grid_chunks
+    r1 = n_total if rank == world - 1 else min(n_total, (rank + 1) * per * cs)
     return r0, r1
 
 
