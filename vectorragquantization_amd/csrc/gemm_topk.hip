@@ -9,13 +9,12 @@
 // stable sorted(..., reverse=True) (:296, :321) over the rows taken in index order.
 //
 // Method (exact for every input):
-//  1. prep: q/S = a + rho (one int8 "piece", S = max|q|/127; the two-piece build adds b/256 with S
-//     a power of two) and rho the exact residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
+//  1. prep: q/S = a + rho (one int8 "piece", S = max|q|/127) and rho the exact residual.  Delta_q bounds |u - s'| over all rows, where u is the matrix-core value below and
 //     s' the reference score in the same units (Phase III: s/S; Phase II: (s + sum q)/(2S)):
 //       Phase III  Delta = ||rho||_2 (Cauchy-Schwarz; the score divides by ||x||_2) + f32 slack
 //       Phase II   Delta = max(sum rho+, sum rho-) (x in {0,1}: <rho, x> lies between them) + f32 slack
 //  2. sample pass (dense): u for every (query, row) of an evenly spread row sample, where
-//     u = fl(A_0 [+ A_1/256]) [* fl(1/||x||)] and A_p = <piece_p, x> are exact i32 MFMA dot products
+//     u = fl(A) [* fl(1/||x||)] and A = <a, x> is an exact i32 MFMA dot product
 //     (x = the int8 row, or the code's bits expanded to 0/1 bytes).  Only the running max of u per
 //     (query, sample chunk, lane row) leaves the kernel: 32 values per query and chunk, each the u
 //     of a distinct sample row (the [nq, S] matrix is never written).
@@ -27,13 +26,14 @@
 //     overflow (heavy ties) or fewer than min(k, n) candidates (zero-norm rows) sends the query to
 //     the exact fallback: one workgroup scans every row.
 //
-// Work decomposition of the two matrix passes: one 256-thread workgroup per CU; each wave holds the
-// int8 piece of 64 queries (two pieces of 32) for all of d = 1024 in the accumulator file (256 AGPRs);
-// 32-row tiles stream HBM -> LDS by LDS-DMA (2-3 tiles ahead, pieces spread over the MFMA shadow) and every B fragment read
-// from LDS feeds two MFMAs (both M-blocks, or both pieces).  Phase III reads the int8 rows as B directly (XOR-swizzled
-// image, conflict-free ds_read_b128); Phase II expands the packed bits into 0/1 bytes once per tile
-// (shared by the four waves) in a fixed k-permutation that the prep kernel applies to the query
-// pieces as well.  The threshold test of tile t-1 runs in tile t's MFMA shadow.
+// Work decomposition of the two matrix passes: one workgroup per CU and 256-query block; the int8
+// pieces of its queries for all of d = 1024 sit in the accumulator file (Phase III: 8 waves of 32
+// queries, two per SIMD; Phase II: 4 waves of 64).  32-row tiles stream HBM -> LDS by LDS-DMA (pieces
+// spread over the MFMA shadow).  Phase III reads the int8 rows as B directly (XOR-swizzled image,
+// conflict-free ds_read_b128); Phase II expands the packed bits into 0/1 bytes once per tile (shared by
+// the four waves) in a fixed k-permutation that the prep kernel applies to the queries as well, and
+// every B fragment feeds both of a wave's M-blocks.  The threshold test of tile t-1 runs in tile t's
+// MFMA shadow.
 #include <math.h>
 #include <stdlib.h>
 
@@ -41,124 +41,42 @@
 #include "mfma_common.h"
 #include "vrq_internal.h"
 
-// tools/build_g5_variants.sh compiles this file with VRQ_G5_BISECT bits set to time the matrix pass
-// with parts removed (1: threshold test, 2: LDS-DMA, 4: tile barrier, 8: MFMA, 16: candidate
-// flush, 32: every other B-fragment read (each fragment feeds two k-steps' MFMAs); 2/4/8/16 give wrong results, timing only) and VRQ_G5_BAHEAD (B fragments read this many k-steps ahead).  Never set in
-// the library build.
-#ifndef VRQ_G5_BISECT
-#define VRQ_G5_BISECT 0
-#endif
-#ifndef VRQ_G5_BAHEAD
-#define VRQ_G5_BAHEAD 2
-#endif
-#ifndef VRQ_G5_NP3
-#define VRQ_G5_NP3 3
-#endif
-#ifndef VRQ_G5_DMA_STRIDE
-#define VRQ_G5_DMA_STRIDE 3  // k-steps between the LDS-DMA pieces of the next-but-one tile
-#endif
-#ifndef VRQ_G5_PIECES
-#define VRQ_G5_PIECES 1
-#endif
-#ifndef VRQ_G5_NORM_REG
-#define VRQ_G5_NORM_REG 0  // Phase III: the tile's norms by a plain global load into registers (1) instead of LDS-DMA
-#endif
-#ifndef VRQ_G5_STAGE
-// thresholded pass: 1 = a tile's hits (at most one per lane: the usual case) go to a per-wave LDS
-// stage by wave-prefix positions (no atomic, no wait), drained into the per-(query, chunk) lists
-// once per chunk; 0 = every hit straight to its list (LDS atomic + wait + global store per hit)
-#define VRQ_G5_STAGE 1
-#endif
-constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave << 26 | chunk row)
-constexpr int64_t kMaxChunkRows = (int64_t(1) << 26) - 32;  // chunk rows fit the stage's 26-bit field
-#ifndef VRQ_G5_SEED
-// Phase-II thresholded pass: the accumulators start at -ceil(thr) (an integer seed per query: the
-// binary u is the integer dot), so a test is one integer max per accumulator register and the flush
-// re-derives the hit bits (acc >= 0) from the still-live accumulators
-#define VRQ_G5_SEED 1
-#endif
-#ifndef VRQ_G5_HIT
-// thresholded pass, per-lane record of the tests of a tile: 3 = Phase III: one wave mask per test
-// (HWM below; Phase II keeps its integer seeds), 2 = a per-lane hit bitmask built by the tests (the
-// flush reads it: no recomputation); 1 = the running max only, the flush recomputes u - thr from the
-// still-live accumulators; 0 = a ures[] register file of the tests' values.  Measured (10M x 1024,
-// nq = 1024, one box, two runs each): Phase-III main pass 8.74 / 8.64 ms (3) vs 8.82 / 8.92 (2)
-#define VRQ_G5_HIT 3
-#endif
-// timing-only probes of the DMA's cost (wrong results): 1 = every tile's DMA reads the chunk's first
-// tile (L2-resident source), 2 = the pieces are plain global loads into a discarded register (no LDS write)
-#ifndef VRQ_G5_DMA_PROBE
-#define VRQ_G5_DMA_PROBE 0
-#endif
-// Phase-III thresholded pass: stage the int8 tiles through registers (global_load_dwordx4 during
-// tile t-1, ds_write_b128 into the image during tile t, for tile t+1) instead of LDS-DMA
-// threshold tests held at their k-steps by a register pin (0: probe builds, the compiler's placement)
-#ifndef VRQ_G5_PIN_TESTS
-#define VRQ_G5_PIN_TESTS 1
-#endif
-// cache policy (aux bits) of the corpus-row LDS-DMA pieces (probe builds: 2 = non-temporal)
-#ifndef VRQ_G5_DMA_AUX
-#define VRQ_G5_DMA_AUX 0
-#endif
-#ifndef VRQ_G5_REGSTAGE
-#define VRQ_G5_REGSTAGE 0
-#endif
-// thresholded pass with hit bitmasks (VRQ_G5_HIT == 2): the k-step of tile t at which tile t-2's hits
-// are flushed (the flush reads only the bitmask, no accumulator, so it can sit in the MFMA shadow);
-// -1 = before the tile's first B read, where it delays the tile's first MFMA
-// Phase-III passes: ring of 3 tiles with ONE barrier per tile at k-step 1 (tile t+1 landed and
-// visible, every wave done with tile t-1's slot, which tile t+2's DMA then refills), so the first B
-// fragments and the norm of tile t+1 are read during tile t's last k-steps: no barrier or LDS
-// latency between two tiles' MFMAs
-#ifndef VRQ_G5_XB
-#define VRQ_G5_XB 0
-#endif
-#ifndef VRQ_G5_FLUSH_STEP
-#define VRQ_G5_FLUSH_STEP 1
-#endif
-
 namespace vrq {
 namespace g5 {
 
-constexpr int GW = 4;                // waves per workgroup (one per SIMD)
-// int8 pieces per query: 2 (q/S = a + b/256 + rho, 16-bit split, 32 queries per wave) or 1 (q/S =
-// a + rho, 64 queries per wave: half the MFMA work and twice the corpus-byte reuse per query, a
-// ~4x wider threshold margin -> ~2K exact rescorings per query at 10M rows).  Either way the A
-// fragments fill the 256 accumulator registers.  Measured at 10M x 1024, nq = 1024 (both phases):
-// one piece 29.3 ms, two pieces 40.6 ms per batch -> one piece is the library build.
-constexpr int NPC = VRQ_G5_PIECES;
-constexpr int NMB = 3 - NPC;         // 32-query M-blocks per wave
-constexpr int GQW = 32 * NMB;        // queries per wave
-constexpr int GQB = GW * GQW;        // queries per workgroup
-constexpr int NE = 16 * NMB;         // threshold tests per lane per tile
-#ifndef VRQ_G5_W8
-// Phase-III passes: 8 waves (two per SIMD) of 32 queries instead of 4 of 64; a SIMD's second wave
-// keeps its matrix core busy while the first issues its threshold tests and LDS-DMA pieces
-// (10M x 1024, nq = 1024: main pass 8.8 vs 9.5 ms, tools/probes)
-#define VRQ_G5_W8 1
-#endif
-#ifndef VRQ_G5_NP3_W8
-#define VRQ_G5_NP3_W8 2  // the 8-wave layout's DMA ring (tile t+1 streamed during tile t)
-#endif
-// wave layout of a matrix pass: W waves of MB 32-query M-blocks (W * 32 * MB = GQB queries per
-// workgroup either way), RPW rows of each 32-row tile streamed per wave
+// Matrix-pass layout: one workgroup per CU and 256-query block, the A fragments of its queries for
+// all of d = 1024 in the accumulator file, one int8 piece per query (q/S = a + rho):
+//   Phase III: 8 waves (two per SIMD) of 32 queries -- a SIMD's second wave keeps its matrix core busy
+//              while the first issues its threshold tests and LDS-DMA pieces (main pass 8.8 vs 9.5 ms
+//              for 4 waves of 64 at 10M x 1024, nq = 1024, round 3);
+//   Phase II:  4 waves of 64 queries, each B fragment feeding both M-blocks.
+// One piece (vs q/S = a + b/256 + rho) halves the MFMA work and doubles the corpus-byte reuse per
+// query at a ~4x wider threshold margin (~2K exact rescorings per query at 10M rows): 29.3 vs 40.6 ms
+// per 10M batch, both phases (round 2).
+constexpr int GQB = 256;  // queries per workgroup
 template <int PH>
 struct KShape {
-  static constexpr bool W8 = PH != VRQ_GEMM_BINARY && VRQ_G5_W8 && NPC == 1;
-  static constexpr int W = W8 ? 8 : GW, MB = W8 ? 1 : NMB, QW = 32 * MB, NE = 16 * MB, RPW = 32 / W;
+  static constexpr bool P3 = PH != VRQ_GEMM_BINARY;
+  static constexpr int W = P3 ? 8 : 4, MB = P3 ? 1 : 2, QW = 32 * MB, NE = 16 * MB, RPW = 32 / W;
   static_assert(W * QW == GQB, "query block");
 };
 // planning target for the candidates per query (the sample size follows from it), and the
-// per-(query, chunk) list capacity as a multiple of the hits the sample predicts (one piece: ~4x
-// wider margin)
-constexpr int FIN_CAP = NPC == 2 ? 4096 : 8192;
-constexpr int CAP_MULT = NPC == 2 ? 4 : 16;
+// per-(query, chunk) list capacity as a multiple of the hits the sample predicts
+constexpr int FIN_CAP = 8192;
+constexpr int CAP_MULT = 16;
+// thresholded pass: a tile's hits (at most one per lane: the usual case) go to a per-wave LDS stage by
+// wave-prefix positions (no atomic, no wait), drained into the per-(query, chunk) lists once per chunk
+constexpr int STG5 = 1024;  // staged hit entries per wave (u32: query-in-wave << 26 | chunk row)
+constexpr int64_t kMaxChunkRows = (int64_t(1) << 26) - 32;  // chunk rows fit the stage's 26-bit field
 constexpr int GRT = 32;              // corpus rows per tile (one 32-column N-block)
 constexpr int GKS = 32;              // k-steps of 32 dims (d = 1024)
 constexpr int T3 = GRT * 1024;       // Phase-III tile: 32 int8 rows (32 KiB) ...
 constexpr int T3N = T3 + GRT * 8;    // ... + their 32 f64 norms
 constexpr int T2 = GRT * 128;        // Phase-II packed tile (4 KiB)
 constexpr int U2 = GKS * 1024;       // Phase-II unpacked tile [k-step][lane][16 B] (32 KiB)
+// tile schedule: B fragments read BA k-steps ahead; the LDS-DMA pieces of the tile AHEAD tiles
+// ahead issue every DS k-steps from k-step 2 (round 3 sweeps of both moved nothing)
+constexpr int BA = 2, DS = 3;
 
 // main-pass chunks per (CU, query block): 4 keeps the query blocks that stream the same chunk
 // within L2 reach of each other (PMC bytes 1.1x algorithmic vs 1.9x at 1, equal time; round 2)
@@ -167,7 +85,7 @@ constexpr int FB_BATCH = 1024;       // rows per batch of the exact fallback
 constexpr int KMAX5 = 1024;          // k bound of the path
 constexpr int64_t kMinSample = 32768;
 constexpr int64_t kMaxSample = 1 << 21;
-constexpr int QA_BYTES = NPC * 1024; // per query: piece 0 (then piece 1), fragment order
+constexpr int QA_BYTES = 1024;       // per query: the int8 piece in fragment order
 
 // Phase-II k-permutation inside a 32-dim k-step: fragment byte j = 4t + b of lane half h holds
 // bit 8b + t + 4h of the little-endian code dword (so a dword of the fragment is (w >> (t+4h)) &
@@ -210,7 +128,7 @@ __device__ __forceinline__ int xcd_logical(int b, int nb) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// prep: one wave per (padded) query.  qa[q] = pieces a, b in fragment order (natural k order for
+// prep: one wave per (padded) query.  qa[q] = the piece a in fragment order (natural k order for
 // Phase III, ph2_pos for Phase II); delta[q] = Delta_q in u units; (alpha[q], beta[q]) map a reference
 // score s to u units (s' = alpha s + beta), for the raised threshold of the retry pass.
 __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* __restrict__ qf, int nq, int nq_pad,
@@ -222,7 +140,6 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   int8_t* o = qa + (int64_t)q * QA_BYTES;
   if (q >= nq) {  // padding queries: zero pieces (their thresholds never accept)
     reinterpret_cast<int4*>(o)[l] = make_int4(0, 0, 0, 0);
-    if (NPC == 2) reinterpret_cast<int4*>(o)[64 + l] = make_int4(0, 0, 0, 0);
     if (l == 0) {
       delta[q] = 0.0;
       alpha[q] = 0.0;
@@ -237,25 +154,15 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
   for (int i = 0; i < DPL; ++i) mx = fmaxf(mx, fabsf(qv[i]));
 #pragma unroll
   for (int m = 1; m < WAVE; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, WAVE));
-  // two pieces: S = 2^e, the smallest power of two with max|q| / S <= 127 (exact scaling in f64);
-  // one piece: S = max|q| / 127 (the rounding of q/S in f64 is far inside the slack below)
-  int e = 0;
-  if (mx > 0.f) {
-    e = (int)ceil(log2((double)mx / 127.0));
-    while ((double)mx > 127.0 * ldexp(1.0, e)) ++e;
-    while ((double)mx <= 127.0 * ldexp(1.0, e - 1)) --e;
-  }
-  const double invS = NPC == 2 ? ldexp(1.0, -e) : (mx > 0.f ? 127.0 / (double)mx : 1.0);
+  // S = max|q| / 127 (the rounding of q/S in f64 is far inside the slack below)
+  const double invS = mx > 0.f ? 127.0 / (double)mx : 1.0;
   double r2 = 0.0, rp = 0.0, rn = 0.0, q2 = 0.0, q1 = 0.0, qs = 0.0;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    const double x = (double)qv[i] * invS;  // exact for two pieces
+    const double x = (double)qv[i] * invS;
     double a = rint(x);                     // |a| <= 127
     a = a > 127.0 ? 127.0 : (a < -127.0 ? -127.0 : a);
-    const double f = x - a;                 // exact, |f| <= 1/2
-    double b = NPC == 2 ? rint(f * 256.0) : 0.0;
-    b = b > 127.0 ? 127.0 : (b < -127.0 ? -127.0 : b);
-    const double rho = f - b * (1.0 / 256.0);  // exact
+    const double rho = x - a;               // exact, |rho| <= 1/2
     r2 += rho * rho;
     rp += rho > 0.0 ? rho : 0.0;
     rn += rho < 0.0 ? -rho : 0.0;
@@ -265,7 +172,6 @@ __global__ __launch_bounds__(256) void gemm_prep_kernel(int mode, const float* _
     const int dim = DPL * l + i, s = dim >> 5;
     const int pos = s * 32 + (mode == VRQ_GEMM_BINARY ? ph2_pos(dim & 31) : (dim & 31));
     o[pos] = (int8_t)a;
-    if (NPC == 2) o[1024 + pos] = (int8_t)b;
   }
   r2 = wave_sum_f64(r2);
   rp = wave_sum_f64(rp);
@@ -311,23 +217,16 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   constexpr bool P3 = PH == VRQ_GEMM_INT8_COSINE;
   constexpr int KW = KShape<PH>::W, KMB = KShape<PH>::MB, KQW = KShape<PH>::QW, KNE = KShape<PH>::NE;
   constexpr int RPW = KShape<PH>::RPW;               // Phase III: tile rows streamed per wave
-  constexpr int NA = NPC == 2 ? 2 : KMB;             // A fragment sets per wave (pieces or M-blocks)
-  // Phase III: ring of 3 raw tiles, tile t+2 streamed in during tile t (9 DMA pieces per wave).
-  // Phase II: ring of 4 packed tiles, tile t+3 streamed in during tile t (1 piece per wave), and the
-  // packed tile t+1 expanded into the unpacked ring (2 tiles) during tile t.
-  // RS (register staging, Phase-III thresholded pass): ring of 2 images; during tile t each wave
-  // writes its 8 staged rows of tile t+1 into the free image and loads its rows of tile t+2
-  constexpr bool RS = P3 && !DENSE && VRQ_G5_REGSTAGE;
-  constexpr bool XB = P3 && !VRQ_G5_REGSTAGE && !VRQ_G5_NORM_REG && VRQ_G5_XB;
-  constexpr int NP = RS ? 2 : XB ? 3 : P3 ? (KShape<PH>::W8 ? VRQ_G5_NP3_W8 : VRQ_G5_NP3) : 4;
+  // Phase III: ring of 2 raw tiles (32 int8 rows + their norms), tile t+1 streamed in during tile t
+  // (5 DMA pieces per wave: 4 rows + the norms).  Phase II: ring of 4 packed tiles, tile t+3 streamed in
+  // during tile t (1 piece per wave), and the packed tile t+1 expanded into the unpacked ring (2 tiles).
+  constexpr int NP = P3 ? 2 : 4;
   constexpr int PKT = P3 ? T3N : T2;                  // ring slot bytes
   constexpr int SMEM = NP * PKT + (P3 ? 0 : 2 * U2);
   constexpr int PPW = P3 ? RPW + 1 : 1;               // vector-memory instructions per wave per tile
-  constexpr bool NREG = P3 && (VRQ_G5_NORM_REG || RS);  // (8 LDS-DMA rows + 1 norm load, or 9 LDS-DMA)
   constexpr int AHEAD = NP - 1;                       // tiles the DMA runs ahead
-  static_assert(!(RS && KShape<PH>::W8), "register staging assumes 4 waves");
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
-  constexpr bool STAGE = !DENSE && VRQ_G5_STAGE;
+  constexpr bool STAGE = !DENSE;
   // per-(query, this chunk) list lengths (one row per wave), then each wave's hit stage
   __shared__ int32_t lcnt[KW * KQW + (STAGE ? KW * STG5 : 0)];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -353,12 +252,12 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     return tiny ? r < nrows : r >= t * GRT - tstart(t);
   };
   // ---- LDS-DMA of tile t (piece i of PPW per wave): a uniform base plus a per-lane offset.
-  //   Phase III: tile row rr = 8w + i -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the
-  //              row; piece 8 = the tile's 32 f64 norms (every wave loads the same 256 B, so the DMA
+  //   Phase III: tile row rr = 4w + i -> slots rr*64 + c', holding 16-B chunk c' ^ (rr & 15) of the
+  //              row; piece 4 = the tile's 32 f64 norms (every wave loads the same 256 B, so the DMA
   //              count per wave is uniform).
   //   Phase II:  rows 8w..8w+7 -> slot rr*8 + c' holding chunk c' ^ ((rr >> 1) & 7).
   const int RB = P3 ? 1024 : 128;  // bytes per corpus row
-  uint32_t loff[P3 ? 8 : 1];
+  uint32_t loff[P3 ? RPW : 1];
   if constexpr (P3) {
 #pragma unroll
     for (int i = 0; i < RPW; ++i) loff[i] = (uint32_t)(i * 1024 + ((l ^ ((RPW * w + i) & 15)) << 4));
@@ -373,7 +272,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     uint8_t* lds;
   };
   auto dma_tile = [&](int t, int slot_i) {  // whole tiles (not tiny)
-    const int64_t tr0 = row0 + (VRQ_G5_DMA_PROBE == 1 ? 0 : tstart(t));
+    const int64_t tr0 = row0 + tstart(t);
     DmaTile d;
     d.gsrc = src + (tr0 + (P3 ? RPW : 8) * w) * RB;
     d.gnrm = reinterpret_cast<const uint8_t*>(norms + tr0);
@@ -390,13 +289,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     }
     const uint8_t* g = d.gsrc + loff[P3 ? i : 0];
     uint8_t* ld = d.lds + (P3 ? (RPW * w + i) * 1024 : w * 1024);
-    if constexpr (VRQ_G5_DMA_PROBE == 2) {
-      v4i sink;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(sink) : "v"(g) : "memory");
-      asm volatile("" ::"v"(sink));
-    } else {
-      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, VRQ_G5_DMA_AUX);
-    }
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
     if (P3 && i == RPW) {
@@ -428,58 +321,29 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     lds_write128(ubw + (uint32_t)(((4 * uc + i) * 64 + hh * 32 + r) * 16), f);
   };
 
-  // NREG: this lane's row norm of a tile (tile row r; both lane halves load the same) into a
-  // register, issued before the tile's 8 row pieces so the per-tile vmcnt accounting is unchanged
-  double nvr[2] = {0.0, 0.0};  // by tile parity: tile t's norm, loaded during tile t - 2
-  auto issue_norm = [&](int tt, double& dst) {
-    const double* base = norms + row0 + tstart(tt);
-    const uint32_t off = (uint32_t)((tiny ? (r < nrows ? r : nrows - 1) : r) * 8);
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(dst) : "v"(off), "s"(base) : "memory");
-  };
   for (int t = 0; t < AHEAD && t < ntiles; ++t) {
-    if constexpr (NREG) {
-      if (t == 0) issue_norm(0, nvr[0]);
-      else issue_norm(1, nvr[1]);
-    }
 #pragma unroll
-    for (int i = 0; i < (NREG ? RPW : PPW); ++i) {
+    for (int i = 0; i < PPW; ++i) {
       if (tiny)
         issue_tiny(i);
       else
         issue_piece(dma_tile(t, t), i);
     }
   }
-  // RS: this wave's 8 rows of the staged tile (tile t+1 during tile t), one 16-B chunk per lane in
-  // the image's order (row 8w+i, chunk l ^ (row & 15): the same image the LDS-DMA fills)
-  v4i stg[RS ? 8 : 1];
-  auto stage_load = [&](int tt, int i) {
-    const uint8_t* base = src + (row0 + tstart(tt) + 8 * w) * RB;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(stg[RS ? i : 0]) : "v"(loff[P3 ? i : 0]), "s"(base) : "memory");
-  };
-  if constexpr (RS) {
-    if (ntiles > 1) {  // (ntiles > 1: no tiny chunk)
-      issue_norm(1, nvr[1]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) stage_load(1, i);
-    }
-  }
 
-  // A fragments of this wave's 32 queries, both pieces, all 32 k-steps -> accumulator file
+  // A fragments of this wave's M-blocks of 32 queries, all 32 k-steps -> accumulator file
   const int qbase = qb * GQB + w * KQW;
-  v4i A[2][GKS];  // [piece] (two pieces) or [M-block] (one piece); NA of them used
-  {
+  v4i A[KMB][GKS];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const int8_t* qp = NPC == 2 ? qa + (int64_t)(qbase + r) * QA_BYTES + j * 1024 + h * 16
-                                  : qa + (int64_t)(qbase + 32 * j + r) * QA_BYTES + h * 16;
+  for (int j = 0; j < KMB; ++j) {
+    const int8_t* qp = qa + (int64_t)(qbase + 32 * j + r) * QA_BYTES + h * 16;
 #pragma unroll
-      for (int s = 0; s < GKS; ++s) A[j][s] = *reinterpret_cast<const v4i*>(qp + s * 32);
-    }
+    for (int s = 0; s < GKS; ++s) A[j][s] = *reinterpret_cast<const v4i*>(qp + s * 32);
   }
 #pragma unroll
-  for (int p = 0; p < NA; ++p)
+  for (int j = 0; j < KMB; ++j)
 #pragma unroll
-    for (int s = 0; s < GKS; ++s) asm volatile("" : "+a"(A[p][s]));
+    for (int s = 0; s < GKS; ++s) asm volatile("" : "+a"(A[j][s]));
   // test e of a lane: M-block e >> 4, accumulator register g = e & 15 -> query row of the wave
   auto qrow = [&](int e) { return 32 * (e >> 4) + ((e & 3) + 8 * ((e >> 2) & 3) + 4 * h); };
   float th[KNE];
@@ -490,8 +354,11 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   // which every tile then executes after issuing its LDS-DMA pieces (waiting for the next tile's DMA)
 #pragma unroll
   for (int e = 0; e < KNE; ++e) asm volatile("" : "+v"(th[e]));
-  constexpr bool SEED2 = !P3 && !DENSE && NPC == 1 && VRQ_G5_SEED;
-  v16i seed[SEED2 ? 2 : 1];  // SEED2: -ceil(thr) of each accumulator register's query, clamped
+  // Phase-II thresholded pass: the accumulators start at -ceil(thr) (an integer seed per query: the
+  // binary u is the integer dot), so a test is one integer max per accumulator register and the flush
+  // re-derives the hit bits (acc >= 0) from the still-live accumulators
+  constexpr bool SEED2 = !P3 && !DENSE;
+  v16i seed[SEED2 ? 2 : 1];  // -ceil(thr) of each accumulator register's query, clamped
   if constexpr (SEED2) {
 #pragma unroll
     for (int e = 0; e < KNE; ++e) {
@@ -511,24 +378,18 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   const uint32_t sg0 = lds_addr(lcnt + KW * KQW + (STAGE ? w * STG5 : 0));  // this wave's hit stage
   int nst = 0;  // staged entries (wave-uniform)
   if (!DENSE && l < KQW) lcnt[w * KQW + l] = 0;  // made visible by the first tile's barrier
-  v16i acc[2][2] = {};   // [tile parity][piece or M-block]
-  // results of the previous tile (flushed at the top of the next-but-one tile): the sample pass
-  // keeps u; the thresholded pass keeps u - thr (a hit iff >= 0; NaN never) and their running max.
-  // UREC: the thresholded pass keeps only the running max; a flush recomputes u - thr from the
-  // tile's accumulators, which stay live until the next-but-one tile's first MFMA.  HMASK: each test
-  // shifts its hit bit into hm (test e -> bit KNE-1-e), the flush reads hm.  Both: no ures[] file.
-  constexpr bool HMASK = !DENSE && VRQ_G5_HIT >= 2;
-  // HWM (VRQ_G5_HIT == 3): test e of a tile leaves its hits as one wave mask (v_cmp into an SGPR
-  // pair: cvt + fma + cmp per test, no per-lane bit assembly); the flush ORs the 16 masks on the
-  // scalar unit and builds per-lane bitmasks only for a tile with a hit
-  constexpr bool HWM = HMASK && P3 && VRQ_G5_HIT == 3;
-  constexpr bool UREC = !DENSE && VRQ_G5_HIT >= 1;
-  float ures[UREC ? 1 : KNE];
-  float umax = -__builtin_inff(), uodd = 0.f;
-  uint32_t hm = 0;
+  v16i acc[2][2] = {};   // [tile parity][M-block]
+  // The sample pass keeps, per (lane, test), the running max of u over the chunk's rows of that lane.
+  // Phase-III thresholded pass: test e of a tile leaves its hits as one wave mask (v_cmp into an SGPR
+  // pair: cvt + fma + cmp per test, no per-lane bit assembly); the flush of tile t-2 ORs the 16 masks
+  // on the scalar unit and builds per-lane bitmasks only for a tile with a hit.  (Measured at 10M x 1024,
+  // nq = 1024, one box, two runs each: main pass 8.74 / 8.64 ms vs 8.82 / 8.92 ms for per-lane hit bits
+  // and 8.99 / 8.95 ms for a recomputation from the still-live accumulators; round 3.)
+  constexpr bool HWM = P3 && !DENSE;
+  float ures[DENSE ? KNE : 1];
   uint64_t hmk[HWM ? KNE : 1] = {};
 #pragma unroll
-  for (int e = 0; e < (UREC ? 1 : KNE); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
+  for (int e = 0; e < (DENSE ? KNE : 1); ++e) ures[e] = DENSE ? __builtin_nanf("") : 0.f;
   float invc = 0.f, invp = 0.f, invpp = 0.f;  // Phase III 1/||x|| of tiles t, t-1, t-2 (NaN: zero norm or past the chunk)
   const v16i zero = {};
   const int64_t qstride = (int64_t)nchunks * capc;
@@ -537,7 +398,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   // the query's threshold in the thresholded pass (one fma for Phase III)
   auto uval = [&](const v16i& a0, const v16i& a1, int e, float inv) {
     const int g = e & 15;
-    const float u = NPC == 2 ? fmaf((float)a1[g], 1.0f / 256.0f, (float)a0[g]) : (float)((e >> 4) ? a1[g] : a0[g]);
+    const float u = (float)((e >> 4) ? a1[g] : a0[g]);
     if constexpr (DENSE)
       return P3 ? u * inv : u;
     else
@@ -562,9 +423,9 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     }
     nst = 0;
   };
-  // results of tile tt (computed in the following tile's shadow) -> HBM; (a0, a1, inv): tile tt's
-  // accumulators and 1/||x|| (UREC)
-  auto flush = [&](int tt, const v16i& a0, const v16i& a1, float inv) {
+  // hits of tile tt (tested in the following tile's shadow) -> the stage; (a0, a1): tile tt's
+  // accumulators (Phase II re-derives its hit bits from them)
+  auto flush = [&](int tt, const v16i& a0, const v16i& a1) {
     const int lr = tstart(tt) + r;
     const bool ok = lane_valid(tt);
     if constexpr (!DENSE) {
@@ -575,35 +436,25 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
         for (int e = 0; e < KNE; ++e) any |= hmk[e];
         fl = any != 0;
       } else {
-        fl = __ballot(SEED2 ? imax >= 0 : HMASK ? hm != 0 : umax >= 0.f) != 0;
+        fl = __ballot(imax >= 0) != 0;
       }
-      if (!(VRQ_G5_BISECT & 16) && fl) {
+      if (fl) {
         uint32_t m = 0;  // (hits: ~k * n / sample rows per query over the corpus)
         if constexpr (SEED2) {
           static_for<0, KNE>([&](auto E) {
             constexpr int e = decltype(E)::value;
             m |= (((e >> 4) ? a1 : a0)[e & 15] >= 0 ? 1u : 0u) << (KNE - 1 - e);
           });
-        } else if constexpr (HWM) {
+        } else {
 #pragma unroll
           for (int e = 0; e < KNE; ++e) {
             uint32_t b;
             asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(b) : "v"(1u << (KNE - 1 - e)), "s"(hmk[e]));
             m |= b;
           }
-        } else if constexpr (HMASK) {
-          m = hm;
-        } else {
-          static_for<0, KNE>([&](auto E) {
-            constexpr int e = decltype(E)::value;
-            if constexpr (UREC)
-              m |= (uval(a0, a1, e, inv) >= 0.f ? 1u : 0u) << (KNE - 1 - e);
-            else
-              m |= (ures[e] >= 0.f ? 1u : 0u) << (KNE - 1 - e);
-          });
         }
         if (!ok) m = 0;
-        if (STAGE && !__ballot((m & (m - 1)) != 0)) {
+        if (!__ballot((m & (m - 1)) != 0)) {
           // at most one hit per lane: one staged entry per hit lane at its rank among them
           const uint64_t lanes = __ballot(m != 0);
           if (m) {
@@ -621,12 +472,10 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
           }
         }
       }
-      umax = -__builtin_inff();
-      hm = 0;
       imax = INT32_MIN;
     }
   };
-  // SEED2 test of accumulator register e of the tested tile (pairs fold into one v_max3_i32)
+  // Phase-II test of accumulator register e of the tested tile (pairs fold into one v_max3_i32)
   auto itest = [&](const v16i& a0, const v16i& a1, int e) {
     const int v = ((e >> 4) ? a1 : a0)[e & 15];
     if (e & 1)
@@ -636,23 +485,13 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   };
   // the sample pass keeps, per (lane, test), the running max of u over the chunk's rows of that
   // lane (NaN: none yet; rows already seen in the previous tile, and Phase-III zero norms, are NaN
-  // and drop out of the max); vp = this lane's row of the tested tile is new
+  // and drop out of the max); vp = this lane's row of the tested tile is new.  Phase-III thresholded
+  // pass: the test's wave mask (NaN: no hit).
   auto test = [&](float u, int e, bool vp) {
-    if constexpr (DENSE) {
+    if constexpr (DENSE)
       ures[e] = fmaxf(ures[e], vp ? u : __builtin_nanf(""));
-    } else if constexpr (HWM) {
-      hmk[e] = __ballot(u >= 0.f);  // NaN: no hit
-    } else if constexpr (HMASK) {
-      hm = (hm << 1) | (u >= 0.f ? 1u : 0u);  // NaN: no hit
-    } else if constexpr (UREC) {
-      if (e & 1)
-        umax = fmaxf(umax, fmaxf(uodd, u));  // pairs fold into one v_max3
-      else
-        uodd = u;
-    } else {
-      ures[e] = u;
-      if (e & 1) umax = fmaxf(umax, fmaxf(ures[e - 1], u));
-    }
+    else
+      hmk[e] = __ballot(u >= 0.f);
   };
 
   if constexpr (!P3) {  // expand tile 0 before the loop (tile t+1 is expanded during tile t)
@@ -667,83 +506,52 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   }
 
   int sl = 0;  // t % NP
-  constexpr int BA = VRQ_G5_BAHEAD;  // B fragments read BA k-steps ahead
-  constexpr int NR = BA < 4 ? 4 : 8; // ring (power of two > BA)
-  static_assert(!XB || (BA >= 1 && BA <= 8 && GKS % NR == 0), "cross-tile B ring");
-  v4i ringx[NR];                     // XB: the B ring and the norm carry over into the next tile
-  double nvx = 0.0;
+  constexpr int NR = 4;  // B fragment ring (power of two > BA)
+  static_assert(BA < NR, "B ring");
   auto tile = [&](auto PAR, auto FIRST, int t) {
     constexpr int p = decltype(PAR)::value;
     constexpr bool first = decltype(FIRST)::value;  // tile 0: no previous tile to test
-    // Phase III: this wave's DMA of tile t landed (only tile t+1's may still be in flight; the
-    // older flush stores too); Phase II: tile t+1's (tile t+2's may be in flight).  After the
-    // barrier every wave's has, the expanded tile t is visible, and every wave is done reading
-    // the slots the DMA of this tile overwrites.
-    if constexpr (XB) {
-      if constexpr (first) {  // tile 0 landed (tile 1's pieces may stay in flight)
-        if (ntiles > 1)
-          wait_vm<PPW>();
-        else
-          wait_vm<0>();
-        barrier_all();
-      }
-    } else if constexpr (RS) {
-      // tile 0: its DMA and norm landed (tile 1's norm + 8 staged rows may stay in flight); later
-      // tiles were written by this wave's ds_writes during the previous tile
-      if (t == 0) {
-        if (ntiles > 1)
-          wait_vm<9>();
-        else
-          wait_vm<0>();
-      }
-      wait_lgkm0();
-    } else {  // the DMA of the tile needed now (t; Phase II: t+1) landed; the INF tiles issued after it may
-              // stay in flight (in the chunk's last tiles: wait for everything)
+    // The DMA of the tile needed now (Phase III: t; Phase II: t+1) landed; the INF tiles issued after
+    // it may stay in flight (in the chunk's last tiles: wait for everything).  After the barrier every
+    // wave's has, the expanded tile t is visible, and every wave is done reading the slots the DMA of
+    // this tile overwrites.
+    {
       constexpr int NEED = P3 ? 0 : 1, INF = AHEAD - 1 - NEED;
       if (t + NEED + INF < ntiles)
         wait_vm<INF * PPW>();
       else
         wait_vm<0>();
     }
-    if (!XB && !(VRQ_G5_BISECT & 4)) barrier_all();
-    // tile t-2's hits (its accumulators are acc[p] until this tile's first MFMA; the bitmask form
-    // needs none of them and flushes at k-step FLS instead)
-    constexpr int FLS = HMASK && !SEED2 ? VRQ_G5_FLUSH_STEP : -1;
-    if (FLS < 0 && !DENSE && t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);
+    barrier_all();
+    // tile t-2's hits: Phase II before the tile's first MFMA (its accumulators are acc[p] until then);
+    // Phase III reads only its wave masks, so its flush sits at k-step FLS = 1, in the MFMA shadow
+    constexpr int FLS = P3 && !DENSE ? 1 : -1;
+    if (FLS < 0 && !DENSE && t >= 2) flush(t - 2, acc[p][0], acc[p][1]);
     const bool vprev = DENSE ? lane_valid(t - 1) : true;  // (the sample pass's test of tile t-1)
     const uint32_t slot = sm0 + (uint32_t)(sl * PKT);
     const bool dma = t + AHEAD < ntiles;
     const DmaTile dt = dma_tile(dma ? t + AHEAD : t, sl == 0 ? NP - 1 : sl - 1);
     const int sl1 = sl + 1 == NP ? 0 : sl + 1;                       // (t + 1) % NP
-    double nvl = 0.0;
-    double& nv = XB ? nvx : nvl;
-    const uint32_t slotn = sm0 + (uint32_t)(sl1 * PKT);  // XB: tile t+1's slot
+    double nv = 0.0;
     v4i pv = {};
     const uint32_t ubn = sm0 + (uint32_t)(NP * T2 + ((t + 1) & 1) * U2);  // Phase II: tile t+1 expanded here
     uint32_t badr[8];
-    if constexpr (NREG) {
-      asm volatile("" : "+v"(nvr[p]));  // landed: older than the tile's row pieces the wait covered
-      nv = nvr[p];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
-    } else if constexpr (P3) {
-      if (!XB || first) lds_read64(nv, slot + T3 + (uint32_t)(r * 8));  // (XB: read during tile t-1)
+    if constexpr (P3) {
+      lds_read64(nv, slot + T3 + (uint32_t)(r * 8));
 #pragma unroll
       for (int j = 0; j < 8; ++j) badr[j] = slot + boff[j];
     } else {
       badr[0] = sm0 + (uint32_t)(NP * T2 + (t & 1) * U2 + l * 16);
     }
-    v4i ringl[NR];
-    v4i(&ring)[NR] = XB ? ringx : ringl;
+    v4i ring[NR];
     auto readB = [&](auto S) {
       constexpr int s = decltype(S)::value;
-      if constexpr ((VRQ_G5_BISECT & 32) && (s & 1)) return;  // probe: half the B reads
       if constexpr (P3)
         lds_read128_off<(s >> 3) * 256>(ring[s & (NR - 1)], badr[s & 7]);
       else
         lds_read128_off<s * 1024>(ring[s & (NR - 1)], badr[0]);
     };
-    if constexpr (!XB || first) static_for<0, BA>([&](auto S) { readB(S); });
+    static_for<0, BA>([&](auto S) { readB(S); });
     VRQ_SCHED_FENCE();
     static_for<0, GKS>([&](auto S) {
       constexpr int s = decltype(S)::value;
@@ -752,71 +560,30 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
         // everything but the BA newest LDS operations is complete: B(s), and the norm (issued
         // before B(0)) / the packed Phase-II tile (issued in step 1, before B(1 + BA))
         asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(ring[s & (NR - 1)]), "+v"(nv), "+v"(pv) : "n"(BA) : "memory");
-      } else if constexpr (XB) {
-        // tile t+1's norm and first B fragments (landed and visible since this tile's barrier)
-        constexpr int sn = s + BA - GKS;
-        if constexpr (sn == 0) lds_read64(nvx, slotn + T3 + (uint32_t)(r * 8));
-        lds_read128_off<(sn >> 3) * 256>(ring[(s + BA) & (NR - 1)], slotn + boff[sn & 7]);
-        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(BA) : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(GKS - 1 - s) : "memory");
       }
-      if constexpr (!(VRQ_G5_BISECT & 8)) {
-        if constexpr (SEED2) {  // tile starts at -ceil(thr) (Phase II, one piece: two M-blocks)
-          acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? seed[0] : acc[p][0]);
-          acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? seed[SEED2 ? 1 : 0] : acc[p][1]);
-        } else {
-          acc[p][0] = mfma_i8(A[0][s], ring[((VRQ_G5_BISECT & 32) ? s & ~1 : s) & (NR - 1)], s == 0 ? zero : acc[p][0]);
-          if constexpr (NA == 2) acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
-        }
-      } else if constexpr (s == 0) {
-        acc[p][0] = ring[0].x + zero;
-        if constexpr (NA == 2) acc[p][1] = ring[0].y + zero;
+      if constexpr (SEED2) {  // tile starts at -ceil(thr) (Phase II: two M-blocks)
+        acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? seed[0] : acc[p][0]);
+        acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? seed[SEED2 ? 1 : 0] : acc[p][1]);
+      } else {
+        acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
+        if constexpr (KMB == 2) acc[p][1] = mfma_i8(A[KMB - 1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
       }
-      if constexpr (NA == 2)
+      if constexpr (KMB == 2)
         asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]));
       else
         asm volatile("" : "+v"(acc[p][0]));
-      if constexpr (XB && s == 1) {
-        // tile t+1 landed (its pieces were issued during tile t-1; none of tile t+2's yet) and is
-        // visible to every wave; every wave is done with tile t-1, whose slot tile t+2 refills
-        wait_vm<0>();
-        if (!(VRQ_G5_BISECT & 4)) barrier_all();
-        VRQ_SCHED_FENCE();
-      }
       if constexpr (s == FLS && !DENSE) {
-        if (t >= 2) flush(t - 2, acc[p][0], acc[p][1], invpp);
+        if (t >= 2) flush(t - 2, acc[p][0], acc[p][1]);
         VRQ_SCHED_FENCE();
       }
       // DMA of tile t + AHEAD, spread over the MFMA shadow
-      if constexpr (RS) {
-        // piece i at k-step 2 + DS*i: write staged row i of tile t+1 (loaded during tile t-1; the 8
-        // operations issued after it -- rows i+1..7 of tile t+1, tile t+2's norm and rows 0..i-1 --
-        // may stay in flight), then load row i of tile t+2 into the same registers
-        constexpr int DS = VRQ_G5_DMA_STRIDE;
-        if constexpr (s >= 2 && s < 2 + DS * 8 && (s - 2) % DS == 0) {
-          constexpr int i = (s - 2) / DS;
-          const bool wr = t + 1 < ntiles, ld = t + 2 < ntiles;
-          if constexpr (i == 0)
-            if (ld) issue_norm(t + 2, nvr[p]);  // (nv holds this tile's norm already)
-          if (wr) {
-            if (ld)
-              asm volatile("s_waitcnt vmcnt(8)" : "+v"(stg[i])::"memory");
-            else
-              asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[i])::"memory");
-            lds_write128(sm0 + (uint32_t)(sl1 * PKT + (8 * w + i) * 1024 + l * 16), stg[i]);
-          }
-          if (ld) stage_load(t + 2, i);
-        }
-      } else if constexpr (P3) {
-        constexpr int DS = VRQ_G5_DMA_STRIDE, NPC3 = NREG ? RPW : RPW + 1;
-        if constexpr (s >= 2 && s < 2 + DS * NPC3 && (s - 2) % DS == 0 && !(VRQ_G5_BISECT & 2)) {
-          if constexpr (NREG && s == 2)
-            if (dma) issue_norm(t + AHEAD, nvr[p]);  // (nv holds this tile's norm already)
+      if constexpr (P3) {
+        if constexpr (s >= 2 && s < 2 + DS * PPW && (s - 2) % DS == 0)
           if (dma) issue_piece(dt, (s - 2) / DS);
-        }
       } else {
-        if constexpr (s == 2 && !(VRQ_G5_BISECT & 2))
+        if constexpr (s == 2)
           if (dma) issue_piece(dt, 0);
         if constexpr (s == 1) lds_read128(pv, sm0 + (uint32_t)(sl1 * T2) + usrc);
         if constexpr (s >= 5 && s < 13) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
@@ -825,7 +592,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
       constexpr int EOFF = KNE == 16 ? 4 : 0;
       if constexpr (s >= EOFF && s < EOFF + KNE) {
         constexpr int e = s - EOFF;
-        if constexpr (!first && !(VRQ_G5_BISECT & 1)) {
+        if constexpr (!first) {
           if constexpr (SEED2)
             itest(acc[p ^ 1][0], acc[p ^ 1][1], e);
           else
@@ -834,20 +601,12 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
           // a use here IR-level sinking gathers all of them after the tile's last MFMAs (past the
           // norm branch at s = 20), one ~90-instruction burst per tile instead of a few instructions
           // in each MFMA gap
-          if constexpr (VRQ_G5_PIN_TESTS) {
-            if constexpr (SEED2)
-              asm volatile("" : "+v"(imax), "+v"(iodd));
-            else if constexpr (DENSE)
-              asm volatile("" : "+v"(ures[e]));
-            else if constexpr (HWM)
-              asm volatile("" : "+s"(hmk[e]));
-            else if constexpr (HMASK)
-              asm volatile("" : "+v"(hm));
-            else if constexpr (UREC)
-              asm volatile("" : "+v"(umax), "+v"(uodd));
-            else
-              asm volatile("" : "+v"(ures[e]), "+v"(umax));
-          }
+          if constexpr (SEED2)
+            asm volatile("" : "+v"(imax), "+v"(iodd));
+          else if constexpr (DENSE)
+            asm volatile("" : "+v"(ures[e]));
+          else
+            asm volatile("" : "+s"(hmk[e]));
         }
       }
       if constexpr (P3 && s == 20) {  // 1/||x|| of this tile's row r (NaN: zero norm or past the end)
@@ -877,9 +636,9 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   const int pl = (ntiles - 1) & 1;
   if (!DENSE && ntiles >= 2) {
     if (pl)
-      flush(ntiles - 2, acc[0][0], acc[0][1], invpp);
+      flush(ntiles - 2, acc[0][0], acc[0][1]);
     else
-      flush(ntiles - 2, acc[1][0], acc[1][1], invpp);
+      flush(ntiles - 2, acc[1][0], acc[1][1]);
   }
   const bool vlast = lane_valid(ntiles - 1);
 #pragma unroll
@@ -900,12 +659,12 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
       if (q < nq) dv[(int64_t)q * dv_stride + (int64_t)chunk * GRT + r] = ures[e];
     }
   } else if (pl) {
-    flush(ntiles - 1, acc[1][0], acc[1][1], invp);
+    flush(ntiles - 1, acc[1][0], acc[1][1]);
   } else {
-    flush(ntiles - 1, acc[0][0], acc[0][1], invp);
+    flush(ntiles - 1, acc[0][0], acc[0][1]);
   }
   if constexpr (!DENSE) {
-    if constexpr (STAGE) drain();
+    drain();
     wait_lgkm0();
     if (l < KQW && qbase + l < nq) ccnt[(int64_t)(qbase + l) * nchunks + chunk] = lcnt[w * KQW + l];
   }
@@ -1071,15 +830,9 @@ __device__ __forceinline__ double score_row(const float (&qv)[DPL], const RowSli
 // 10M rows (c5 finish, ms per 1024 queries; profiles/r2s3/c5_finish_score_batch.jsonl):
 //   binary  1 row 0.89, 2 rows 0.78, 3 rows 0.75, 8 rows 1.25
 //   cosine  1 row 1.23, 2 rows 1.13, 3 rows 1.15, 8 rows 1.79
-// (more rows per round cost VGPRs and with them resident workgroups per CU).  VRQ_G5_SCORE_BATCH
-// overrides it in probe builds (tools/build_g5_variants.sh).
+// (more rows per round cost VGPRs and with them resident workgroups per CU).
 template <int PH>
-constexpr int kScoreBatch =
-#ifdef VRQ_G5_SCORE_BATCH
-    VRQ_G5_SCORE_BATCH;
-#else
-    PH == VRQ_GEMM_BINARY ? 3 : 2;
-#endif
+constexpr int kScoreBatch = PH == VRQ_GEMM_BINARY ? 3 : 2;
 
 // Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
@@ -1144,11 +897,8 @@ constexpr int MAX_CHUNKS = 2048;  // per-query candidate lists the finish kernel
 // finish: threads per query (one workgroup each).  Measured at 10M rows, nq = 1024 (~1.8K Phase-III /
 // ~1.3K Phase-II candidates per query, evenly spread: p99 / mean 1.2-1.4, tools/c5_candidates.py):
 // 256 threads 0.86 / 0.51 ms, 512 threads 0.80 / 0.47 ms, 1024 threads 0.93 / 0.58 ms (Phase III /
-// Phase II; profiles/r3_c5_finish_variants.jsonl).  VRQ_G5_FIN_NT overrides it in probe builds.
-#ifndef VRQ_G5_FIN_NT
-#define VRQ_G5_FIN_NT 512
-#endif
-constexpr int FIN_NT = VRQ_G5_FIN_NT, FIN_NW = FIN_NT / WAVE;
+// Phase II; profiles/r3_c5_finish_variants.jsonl).
+constexpr int FIN_NT = 512, FIN_NW = FIN_NT / WAVE;
 struct FinShared {
   uint64_t key[KMAX5 + FB_BATCH];
   uint32_t row[KMAX5 + FB_BATCH];
@@ -1229,10 +979,6 @@ __global__ __launch_bounds__(FIN_NT) void gemm_finish_kernel(const Rows c, int64
   __syncthreads();
   const int total = sh.pre[nchunks];
   const int need = (int)((int64_t)k < n ? k : n);
-#ifdef VRQ_G5_DEBUG
-  if (tid == 0 && (sh.misc[1] || total < need || q < 4))
-    printf("q %d retry %d candidates %d overflow %d capc %d\n", q, (int)RETRY, total, sh.misc[1], capc);
-#endif
   if (total < need || (RETRY && sh.misc[1])) {
     if (tid == 0) {
       fb_flag[q] = 1;
@@ -1442,7 +1188,7 @@ __global__ __launch_bounds__(256) void flat_ip_prepare_kernel(const float* __res
 using namespace vrq;
 using namespace vrq::g5;
 
-extern "C" int vrq_gemm_topk_pieces(void) { return NPC; }
+extern "C" int vrq_gemm_topk_pieces(void) { return 1; }
 
 namespace {
 
