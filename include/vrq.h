@@ -141,6 +141,14 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
 #define VRQ_SCAN_KIND_VALU 0
 #define VRQ_SCAN_KIND_MFMA 1
 int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* prefix_rows);
+/* Host-only planning introspection of the matrix-core scan (no reference counterpart; tests and
+ * tools): info i64[12] = row-split kernel (1) or shared-tile kernel (0), M-blocks (32 queries) per
+ * wave, chunk rows, chunks, per-(query, chunk) list capacity, workspace offsets of
+ * the candidate lists (u64 keys (v + 1025) << 40 | row, v = dist - tau), of the list lengths (i32
+ * [nq][chunks]) and of tau_s / tau_p / rerun (i32 [nq] each, 256-B aligned), sample rows, sampled
+ * order j, offset of the sorted K-lists, workspace bytes.  VRQ_EUNSUPPORTED when the shape takes the
+ * wavefront scan. */
+int vrq_scan_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* info);
 
 /* ---------------------------------------------------------------------------
  * Merge of per-shard candidate tuples after the RCCL all-gather (multi-GPU

@@ -140,3 +140,37 @@ def test_gemm_plan_chunk_rows_fit_the_hit_stage():
                 assert info[6] == lib.vrq_gemm_topk_workspace_size(mode, n, 1024, nq, 10)
     assert lib.vrq_gemm_topk_plan(3, 1 << 32, 1024, 1, 10, info.ctypes.data) == N.VRQ_EUNSUPPORTED
     assert lib.vrq_gemm_topk_plan(1, 1000, 1024, 1, 10, info.ctypes.data) == N.VRQ_EUNSUPPORTED
+
+
+def test_no_dropped_kernel_stubs():
+    """Every kernel the host code launches has its launch stub in the library: hipcc's host-side
+    compile can drop a template kernel's stub without a diagnostic (a compound pointer expression
+    in an LDS-DMA builtin did, round 4), which only shows as an unresolved symbol at load time."""
+    import subprocess
+    N.load()
+    for lib in (N.lib_path(), N._build.PROBE_LIB):
+        if not os.path.exists(lib):
+            continue
+        nm = subprocess.run(["nm", "-DC", lib], capture_output=True, text=True).stdout
+        undefined = [ln for ln in nm.splitlines() if " U " in ln and "vrq::" in ln]
+        assert not undefined, undefined[:3]
+
+
+def test_no_copies_of_inflight_lds_reads(tmp_path):
+    """No kernel copies (or overwrites) a register that an inline-asm LDS read has not yet filled:
+    the register allocator may move such a value with a v_mov placed before the s_waitcnt that
+    retires the read (round 4: K1r's next-n-block rows, ~1 in 10^4 candidates with a wrong distance
+    on the GPU).  Checked on the disassembly of every built object (tests/isa_check.py)."""
+    import glob
+    import shutil
+    import isa_check
+    N.load()
+    objs = sorted(glob.glob(os.path.join(N._build.OBJDIR, "*.o")))
+    if not objs or not os.path.exists(os.path.join(isa_check.LLVM_BIN, "llvm-objdump")):
+        pytest.skip("no built objects or no ROCm llvm tools")
+    if not shutil.which("objcopy") and not os.path.exists(os.path.join(isa_check.LLVM_BIN, "llvm-objcopy")):
+        pytest.skip("no objcopy")
+    bad = []
+    for o in objs:
+        bad += isa_check.copies_of_inflight_lds_reads(isa_check.disassemble(o, str(tmp_path)))
+    assert not bad, [f"{k}: {i} <- {ld}" for k, i, ld in bad[:4]]

@@ -61,6 +61,7 @@ SIGNATURES = {
     "vrq_search3_finish": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _I32, _I32,
                                      _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "vrq_scan_kind": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
+    "vrq_scan_plan": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
     "vrq_merge_shards": (C.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "vrq_rescore_binary": (C.c_int, [_P, _I32, _I32, _P, _I64, _P, _I32, _P, _P]),
     "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),

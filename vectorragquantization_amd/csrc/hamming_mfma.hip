@@ -34,47 +34,6 @@
 #include "vrq_internal.h"
 #include "vrq_scan.h"
 
-// tools/probes/mfma_bisect.hip compiles this file with VRQ_BISECT bits set to time the kernel
-// with parts removed (1: epilogue, 2: unpack, 4: MFMA, 8: tile barrier, 16: B-fragment waits;
-// 8 and 16 give wrong results, timing only).  Never set in the library build.
-#ifndef VRQ_BISECT
-#define VRQ_BISECT 0
-#endif
-// hit extraction of a flagged (M-block, n-block): 1 = per-lane 16-bit hit masks and one staged
-// entry per lane when no lane holds two hits (the usual case), the 16-ballot walk otherwise;
-// 2 = the same with register-tagged seeds (below): the two-hit check is one ballot per register
-// folded by scalar carry-save ORs, and the hit's query row comes from its value's tag, not a mask;
-// 0 = always the 16-ballot walk.  Measured (profiles/r3_k1m_hit_tag_ab.txt): 1 beats 2 (c2 matrix
-// pass 0.39 vs 0.45 ms, c4 29.1 vs 29.6 ms), so 2 stays a probe-build option.
-// Thresholded passes: exact partial-distance pruning.  After k-steps 0..PK-1 (code bytes 0..8*PK-1)
-// the accumulator of (query q, row r) is A1 = tau'(q)/2 + <q, r>_1, and the rest of the dot is at
-// most pc_2(r), the popcount of the row's remaining bytes, so the row can still be a hit only if
-// A1 > (pc_1(r) - pc_2(r))/2 <= pc(r)/2.  An (M-block, n-block) pair where no lane's register
-// passes that bound skips its remaining MFMAs: its accumulators stay <= pc(r)/2 and the hit test
-// rejects them, so the candidates are exactly those of the full pass.  The row popcounts carry
-// pc_2 in their upper 16 bits.  0 = off.
-#ifndef VRQ_PRUNE
-#define VRQ_PRUNE 0
-#endif
-#ifndef VRQ_PRUNE_K
-#define VRQ_PRUNE_K 10  // even (a 16-byte piece boundary of the packed row)
-#endif
-// probe builds: 1 = the prune test and the per-MFMA branches run but never skip; 2 = the test runs,
-// every MFMA is issued (no branch)
-#ifndef VRQ_PRUNE_DIAG
-#define VRQ_PRUNE_DIAG 0
-#endif
-static_assert(VRQ_PRUNE_K % 2 == 0 && VRQ_PRUNE_K > 0 && VRQ_PRUNE_K < 16, "prune k-step");
-#ifndef VRQ_HIT_FAST
-#define VRQ_HIT_FAST 1
-#endif
-// Register-tagged seeds (VRQ_HIT_FAST == 2, thresholded passes): accumulator register g starts at
-// tau'/2 - 1/4 + g/1024 instead of tau'/2.  The untagged accumulator A = <q,r> + tau'/2 and the
-// threshold pc(r)/2 are multiples of 1/2, so A - 1/4 + g/1024 > pc(r)/2  <=>  A > pc(r)/2 (every
-// test unchanged), all values stay exact in f32 (|A| < 2^11, steps of 2^-10), the largest register
-// of a lane carries its own index g = (int(1024 x) & 511) - 256, and dist - tau = floor(pc - 2x).
-constexpr bool kHitTag = VRQ_HIT_FAST == 2;
-
 namespace vrq {
 
 constexpr int MWAVES = 4;                   // waves per workgroup (one per SIMD)
@@ -82,22 +41,11 @@ constexpr int RT = 64;                      // rows per tile (2 n-blocks of 32)
 constexpr int KS = 16;                      // k-steps of 64 bits (1024-bit codes)
 constexpr int NG = 2 * KS;                  // k-step groups per tile (n-block, k-step)
 constexpr int PKT = RT * 128;               // packed tile bytes (8 KiB)
-#ifndef VRQ_NPK
-#define VRQ_NPK 4
-#endif
-constexpr int NPK = VRQ_NPK;                // packed ring depth (DMA issued NPK tiles ahead)
+constexpr int NPK = 4;                      // packed ring depth (DMA issued NPK tiles ahead)
 constexpr int NUB = 3;                      // unpacked ring: tile t read, t+1 ready, t+2 written
 constexpr int UBT = NG * 1024;              // unpacked tile bytes (32 KiB)
 constexpr int GPW = (PKT / 1024) / MWAVES;  // LDS-DMA instructions per wave per tile (2)
-#if VRQ_BISECT & 16
-#define VRQ_BWAIT "; no wait %7"
-#else
-#define VRQ_BWAIT "s_waitcnt lgkmcnt(%7)"
-#endif
-#ifndef VRQ_BAHEAD
-#define VRQ_BAHEAD 3
-#endif
-constexpr int BAHEAD = VRQ_BAHEAD;          // B fragments read this many groups ahead
+constexpr int BAHEAD = 3;                   // B fragments read this many groups ahead
 constexpr int NRING = BAHEAD < 4 ? 4 : 8;   // B fragment ring (power of two > BAHEAD)
 constexpr int STG = 512;                    // per-wave staged hit entries (u32)
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
@@ -236,8 +184,6 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
-  constexpr bool PRUNE = !DENSE && VRQ_PRUNE;
-  constexpr int PK = VRQ_PRUNE_K;
   constexpr int QPW = MfmaShape<MB>::QPW, QPB = MfmaShape<MB>::QPB;
   __shared__ __attribute__((aligned(16))) uint8_t smem[MfmaShape<MB>::SMEM];
   uint8_t* pk = smem;                                       // NPK packed tiles
@@ -313,16 +259,14 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   }
   // row popcounts: tile rows 16w..16w+15, 4 lanes per row, 2 pieces each
   const int pr = 16 * w + (l >> 2), pc0 = 2 * (l & 3);
-  // PRUNE: weights of this lane's two pieces in the packed (pc | pc_2 << 16) row popcount
-  const int pwa = PRUNE && pc0 >= PK / 2 ? 65537 : 1, pwb = PRUNE && pc0 + 1 >= PK / 2 ? 65537 : 1;
   const uint32_t psrc0 = (uint32_t)(pk_slot(pr, pc0) * 16), psrc1 = (uint32_t)(pk_slot(pr, pc0 + 1) * 16);
   auto unpack_write = [&](const v2i& v, int u, uint32_t ubuf) __attribute__((always_inline)) {
     lds_write128(ubuf + udst[u], unpack_row32((uint32_t)v.x));
     lds_write128(ubuf + udst[u] + 1024, unpack_row32((uint32_t)v.y));
   };
   auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) __attribute__((always_inline)) {
-    int pc = (__popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w)) * pwa +
-             (__popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w)) * pwb;
+    int pc = (__popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w)) +
+             (__popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w));
     pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
     pc += __builtin_amdgcn_update_dpp(0, pc, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
     if ((l & 3) == 0) lds_write32(pbuf + (uint32_t)(pr * 4), pc);
@@ -366,8 +310,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int m = 0; m < MB; ++m)
     if (l < 32) {  // lane l writes [m][h = l >> 4][g = l & 15]
       const int g = l & 15, hh = l >> 4;
-      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh] +
-                       (kHitTag && !DENSE ? (float)g * (1.0f / 1024.0f) - 0.25f : 0.0f);
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
     }
   const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64);  // this lane half's 16 seeds of M-block 0
   auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
@@ -477,7 +420,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
           // acc = <q,r> + tau'/2 with tau' = tau(q) - pc(q), so pc(r) - 2 acc = dist - tau(q) in
           // [-1025, -1] for a hit (exact integers): no per-query value to fetch on this path
-          const int v = kHitTag ? (int)floorf((float)pc - 2.0f * a[g]) : pc - (int)(2.0f * a[g]);
+          const int v = pc - (int)(2.0f * a[g]);
           const int pos = nst + below < STG ? nst + below : STG;
           lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
         }
@@ -490,66 +433,33 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // largest register (the others are <= hp), found by a max3 tree, its query row by the mask's
   // lowest bit -- at its rank among the hit lanes.  Otherwise the 16-ballot walk above.
   auto block_hits_fast = [&](const v16f& a, int m, int pc, float hp, int rel7) __attribute__((always_inline)) {
-    if constexpr (!VRQ_HIT_FAST) {
+    uint32_t m16 = 0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) m16 |= (a[g] > hp ? 1u : 0u) << g;
+    if (__ballot((m16 & (m16 - 1)) != 0)) {  // some lane holds two or more hits (rare)
       block_hits(a, m, pc, hp, rel7);
-    } else if constexpr (kHitTag) {
-      // lanes with >= 1 hit (ones) and with >= 2 (twos): one ballot per register, scalar ORs
-      uint64_t ones = 0, twos = 0;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const uint64_t b = __ballot(a[g] > hp);
-        twos |= ones & b;
-        ones |= b;
-      }
-      if (twos) {  // some lane holds two or more hits (rare)
-        block_hits(a, m, pc, hp, rel7);
-      } else {
-        if ((ones >> l) & 1) {
-          const v16i b = __builtin_bit_cast(v16i, a);  // >= 0 patterns order like their floats
-          const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
-          const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
-          const float mx = __int_as_float(max(max(max(x0, x1), x2), max(max(x3, x4), b[15])));
-          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(ones >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ones, 0));
-          int lo = l;
-          asm volatile("" : "+v"(lo));
-          const int g = ((int)(mx * 1024.0f) & 511) - 256;  // the tag of the lane's single hit
-          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
-          const int v = (int)floorf((float)pc - 2.0f * mx);
-          const int pos = nst + below < STG ? nst + below : STG;
-          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
-        }
-        nst += __popcll(ones);
-      }
     } else {
-      uint32_t m16 = 0;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) m16 |= (a[g] > hp ? 1u : 0u) << g;
-      if (__ballot((m16 & (m16 - 1)) != 0)) {  // some lane holds two or more hits (rare)
-        block_hits(a, m, pc, hp, rel7);
-      } else {
-        const uint64_t lanes = __ballot(m16 != 0);
-        if (m16) {
-          const v16i b = __builtin_bit_cast(v16i, a);  // >= 0 patterns order like their floats
-          const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
-          const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
-          const float mx = __int_as_float(max(max(max(x0, x1), x2), max(max(x3, x4), b[15])));
-          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0));
-          int lo = l;
-          asm volatile("" : "+v"(lo));
-          const int g = __builtin_ctz(m16);
-          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
-          const int v = pc - (int)(2.0f * mx);
-          const int pos = nst + below < STG ? nst + below : STG;
-          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
-        }
-        nst += __popcll(lanes);
+      const uint64_t lanes = __ballot(m16 != 0);
+      if (m16) {
+        const v16i b = __builtin_bit_cast(v16i, a);  // >= 0 patterns order like their floats
+        const int x0 = max(max(b[0], b[1]), b[2]), x1 = max(max(b[3], b[4]), b[5]), x2 = max(max(b[6], b[7]), b[8]);
+        const int x3 = max(max(b[9], b[10]), b[11]), x4 = max(max(b[12], b[13]), b[14]);
+        const float mx = __int_as_float(max(max(max(x0, x1), x2), max(max(x3, x4), b[15])));
+        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0));
+        int lo = l;
+        asm volatile("" : "+v"(lo));
+        const int g = __builtin_ctz(m16);
+        const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+        const int v = pc - (int)(2.0f * mx);
+        const int pos = nst + below < STG ? nst + below : STG;
+        lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (rel7 - ri + (lo & 31)));
       }
+      nst += __popcll(lanes);
     }
   };
   auto row_pc = [&](int pcv, int lr) __attribute__((always_inline)) {  // past the end: no hit
-    return lr < nrows ? (PRUNE ? pcv & 0xffff : pcv) : 0x40000000;
+    return lr < nrows ? pcv : 0x40000000;
   };
   // DENSE: the 16 values v = dist - pc(q) of block (m, n-block) (row lr of the chunk) fold into this
   // lane's running minima; only those leave the kernel (dense_out)
@@ -567,9 +477,6 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   for (int m = 0; m < MB; ++m) hitm[m] = 0;
   int hpb = 0;   // the previous n-block's per-lane threshold pc(r)/2, as float bits
   v16f acc[2][MB];  // [n-block][m]
-  bool live[MB];     // PRUNE: (M-block, current n-block) may still hold a hit after k-step PK - 1
-#pragma unroll
-  for (int m = 0; m < MB; ++m) live[m] = true;
   if constexpr (!DENSE)
     static_for<0, MB>([&](auto M) {
       constexpr int m = decltype(M)::value;
@@ -609,7 +516,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       }
       // everything but the BAHEAD most recent LDS operations has completed: the fragment of
       // this group (read BAHEAD groups ago), the packed unit read 5 groups ago, the popcounts
-      asm volatile(VRQ_BWAIT
+      asm volatile("s_waitcnt lgkmcnt(%7)"
                    : "+v"(ring[gi & (NRING - 1)]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb), "+v"(fe)
                    : "n"(BAHEAD)
                    : "memory");
@@ -623,9 +530,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       //   row popcounts (gi = 28): 4 + 4 bcnt, the lane-quad sums, the LDS write
       //   accumulator re-seeds (j = 4+MB .. 3+2MB... one M-block per group, one read per slot)
       //   asynchronous hit flush (gi = 20+MB and 24+MB, slot 3)
-      constexpr bool TEST = !(VRQ_BISECT & 1) && !DENSE && j >= 2 && j < 2 + MB;
+      constexpr bool TEST = !DENSE && j >= 2 && j < 2 + MB;
       constexpr int tm = TEST ? j - 2 : 0;
-      constexpr bool UNPACK = (gi & 7) == 6 && !(VRQ_BISECT & 2);
+      constexpr bool UNPACK = (gi & 7) == 6;
       constexpr bool SEED = !DENSE && j >= 4 + MB && j < 4 + 2 * MB;
       constexpr int sm = SEED ? j - 4 - MB : 0;
       int e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, f0 = 0;
@@ -651,7 +558,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             hitm[tm] = __ballot(max(max(e3, e4), max(bb[15], f0)) > hpb);
           }
         }
-        if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 1 && k == 0) {
+        if constexpr (!DENSE && j == 1 && k == 0) {
           // the n-block's threshold pc(r)/2 as float bits (>= 0); no previous n-block before tile 0:
           // a threshold no accumulator exceeds
           const int pcr_ = nbk == 0 ? pcvP : pcv[0];
@@ -676,7 +583,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             lds_write128(ubw + udst[gi >> 3] + (uint32_t)(half * 1024), r);
           }
         }
-        if constexpr (gi == 28 && !(VRQ_BISECT & 2)) {  // row popcounts of tile t+2
+        if constexpr (gi == 28) {  // row popcounts of tile t+2
           if constexpr (k == 0) {
             pc0 = __popc(pa.x) + __popc(pa.y) + __popc(pa.z) + __popc(pa.w);
             asm volatile("" : "+v"(pc0));
@@ -684,7 +591,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
             asm volatile("" : "+v"(pc1));
           } else if constexpr (k == 2) {
-            pc0 = PRUNE ? pc0 * pwa + pc1 * pwb : pc0 + pc1;
+            pc0 = pc0 + pc1;
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
             asm volatile("" : "+v"(pc0));
           } else {
@@ -702,7 +609,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           x[4 * k + 3] = piece.w;
           acc[nbk ^ 1][sm] = __builtin_bit_cast(v16f, x);
         }
-        if constexpr (DENSE && !(VRQ_BISECT & 1) && j >= 2 && j < 2 + MB && k == 0) {
+        if constexpr (DENSE && j >= 2 && j < 2 + MB && k == 0) {
           if (nbk == 1 || t > 0) {
             const int pcr_ = nbk == 0 ? pcvP : pcv[0];
             const int lr = (nbk == 0 ? (t - 1) * RT + 32 : t * RT) + ri;
@@ -719,7 +626,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           if constexpr (gi == 24 + MB && !DENSE)  // step 2 (idle lanes add 0)
             lds_add_rtn32(fpos, lc0 + (uint32_t)(((fe >> ENT_Q_SHIFT) & 127) * 4), l < nfl ? 1 : 0);
           // hit extraction of the previous n-block's flagged M-blocks, once per n-block (rare)
-          if constexpr (!DENSE && !(VRQ_BISECT & 1) && j == 3 + MB) {
+          if constexpr (!DENSE && j == 3 + MB) {
             // (hitm[m] is assigned by every n-block's test of M-block m before this point)
             uint64_t any = hitm[0];
 #pragma unroll
@@ -737,39 +644,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           }
         }
       };
-      // PRUNE: this n-block's per-lane bound (pc_1 - pc_2)/2 (rows past the end: never live)
-      float hp1 = 0.f;
-      if constexpr (PRUNE && s == PK) {
-        const int v = pcv[nbk];
-        const int lr = t * RT + 32 * nbk + ri;
-        hp1 = lr < nrows ? 0.5f * (float)((v & 0xffff) - 2 * (v >> 16)) : 3.0e9f;
-      }
       static_for<0, MB>([&](auto M) {
         constexpr int m = decltype(M)::value;
         if constexpr (s == 0 && !DENSE)  // the seeds loaded after the block's last epilogue have landed
           asm volatile("" : "+v"(acc[nbk][m]));
-        if constexpr (PRUNE && s == PK) {  // any lane / register of (m, n-block) above its bound
-          const v16f& a = acc[nbk][m];
-          const float x0 = fmaxf(fmaxf(a[0], a[1]), a[2]), x1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
-          const float x2 = fmaxf(fmaxf(a[6], a[7]), a[8]), x3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
-          const float x4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
-          const float mx = fmaxf(fmaxf(fmaxf(x0, x1), x2), fmaxf(fmaxf(x3, x4), a[15]));
-          live[m] = __ballot(mx > hp1) != 0;
-          if constexpr (VRQ_PRUNE_DIAG == 1) {
-            int one = 1;
-            asm volatile("" : "+s"(one));
-            live[m] = live[m] || one != 0;
-          } else if constexpr (VRQ_PRUNE_DIAG == 2) {
-            int lv = live[m];
-            asm volatile("" ::"s"(lv));
-          }
-        }
-        if constexpr (PRUNE && s >= PK && VRQ_PRUNE_DIAG != 2 && !(VRQ_BISECT & 4)) {
-          if (live[m]) acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], acc[nbk][m]);
-        } else if constexpr (!(VRQ_BISECT & 4))
-          acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], (s == 0 && DENSE) ? v16f{} : acc[nbk][m]);
-        else if constexpr (s == 0 && DENSE)
-          acc[nbk][m] = v16f{};
+        acc[nbk][m] = mfma_fp4(A[m][s], ring[gi & (NRING - 1)], (s == 0 && DENSE) ? v16f{} : acc[nbk][m]);
         // pin the accumulator here: the MFMA intrinsics are pure, and without a use at this
         // point IR-level sinking moves them past the scheduling fences
         asm volatile("" : "+v"(acc[nbk][m]));
@@ -794,10 +673,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     fbase = row0 + (int64_t)(t - 1) * RT;
     if (nst > 64) flush_from(64, fbase);  // rare: more than 64 hits in one tile
     nst = 0;
-    if (!(VRQ_BISECT & 8)) barrier_all();  // B_{t+1}
+    barrier_all();  // B_{t+1}
   }
   store_flushed();
-  if (ntiles > 0 && !(VRQ_BISECT & 1)) {  // n-block 1 of the last tile
+  if (ntiles > 0) {  // n-block 1 of the last tile
     const int lr = (ntiles - 1) * RT + 32 + ri;
     const int pc = row_pc(pcvP, lr);
     const float hp = 0.5f * (float)pc;
@@ -824,7 +703,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 // K1r: the matrix-core scan for SMALL batches (nq <= 128): every wave streams its own rows.
 //
 // With few queries a row tile feeds few MFMAs, so sharing the unpacked tile between the four
-// waves of a workgroup (K1m) no longer pays for its barrier and LDS traffic: here each wave owns a
+// waves of a workgroup (K1m) does not pay for its barrier and LDS traffic: here each wave owns a
 // contiguous chunk of rows, LDS-DMAs its own packed tiles (ring of NPR per wave, no barrier), and
 // unpacks each 32-bit piece of a row straight into the B fragment registers of one k-step.  All MB
 // M-blocks (32 queries each, MB*32 >= nq) of the batch are in every wave.
@@ -832,34 +711,30 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 //   the row: 4 conflict-free ds_read_b128 through the tile swizzle), queries the same dword.
 // Same thresholds (sampled tau_s / exact re-run with tau_p), same per-(query, chunk) lists and
 // suffix merge as K1m; the hit path flushes synchronously (hits are rare at the sizes this serves).
-// Workgroups per CU of the MB = 1 instance (VRQ_K1R_OCC, probe builds): 2 puts two waves on every
-// SIMD (each at <= 256 VGPR + AGPR, a ring of 2 tiles per wave so two workgroups fit the LDS), so one
-// wave's MFMAs run while the other waits on its tile or unpacks.  MB = 2 would spill at 256 registers
-// (its sample pass keeps 32 lane minima besides 64 accumulators) and MB = 4 needs the whole register
-// file: both keep one wave per SIMD.
-#ifndef VRQ_K1R_OCC
-#define VRQ_K1R_OCC 2
-#endif
-template <int MB>
-constexpr int k1r_occ() { return MB == 1 ? VRQ_K1R_OCC : 1; }
-template <int MB>
-constexpr int k1r_npr() { return k1r_occ<MB>() == 2 ? 2 : 3; }  // per-wave packed ring depth
-constexpr int NPR_MAX = 3;  // (tile t+NPR-1 in flight while tile t is read)
-// cache-policy bits of K1r's LDS-DMA: 2 = nt (each row is read by one wave once per batch).  c3
-// (100M rows, nq = 8): 2.11 -> 2.02 ms per pass, 0.76 -> 0.79 of HBM (profiles/r2s3/c3_k1r_nt.txt)
-#ifndef VRQ_K1R_AUX
-#define VRQ_K1R_AUX 2
-#endif
+// MB = 1 runs two workgroups per CU (two waves per SIMD at <= 256 VGPR + AGPR, a ring of 2 tiles per
+// wave), so one wave's MFMAs run while the other waits on its tile or unpacks; MB = 2 / 4 need more
+// than 256 registers and keep one wave per SIMD with a ring of 3 tiles.
+//
+// Registers an LDS read (inline asm: the compiler cannot see when it lands) writes are never copied
+// before the wait that retires it: the packed rows of the next n-block go to the register set of
+// the other parity (rb[par ^ 1], consumed in place by the next n-block, no cur = nxt copy the
+// register allocator could hoist above the wait), and every such register is an operand of that
+// wait.  (Round 4: a v_mov of in-flight rows placed before the s_waitcnt gave wrong distances on
+// ~1 in 10^4 candidates; tests/test_capi.py::test_no_copies_of_inflight_lds_reads checks the ISA.)
 template <int MB>
 struct RowsShape {
+  static_assert(MB == 1 || MB == 2 || MB == 4, "M-blocks per wave");
   static constexpr int QPW = 32 * MB;
-  static constexpr int NPR = k1r_npr<MB>();
+  static constexpr int OCC = MB == 1 ? 2 : 1;  // workgroups (of MWAVES single-wave chunks) per CU
+  static constexpr int NPR = MB == 1 ? 2 : 3;  // packed ring depth per wave (tile t+NPR-1 in flight)
+  static constexpr bool SEEDREG = MB <= 2;     // accumulator seeds kept in registers (else re-read from LDS)
   static constexpr int SMEM = MWAVES * (NPR * PKT + QPW * 8 + (STG + 1) * 4 + MB * 128);
-  static_assert(SMEM * k1r_occ<MB>() <= 160 * 1024, "LDS budget");
+  static_assert(SMEM * OCC <= 160 * 1024, "LDS budget");
 };
+constexpr int K1R_AUX = 2;  // cache policy of the row DMA: nt (each row is read by one wave once per batch)
 
 template <int MODE, int MB>
-__global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_kernel(
+__global__ __launch_bounds__(MWAVES * 64, RowsShape<MB>::OCC) void hamming_mfma_rows_kernel(
     const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
@@ -869,15 +744,16 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
   constexpr int QPW = RowsShape<MB>::QPW;
   constexpr int NPR = RowsShape<MB>::NPR;
+  constexpr bool SEEDREG = RowsShape<MB>::SEEDREG;
   if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
   __shared__ __attribute__((aligned(16))) uint8_t smem[RowsShape<MB>::SMEM];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* pk = smem + w * (NPR * PKT);                                       // this wave's ring
-  int32_t* lcnt = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + w * QPW;
-  int32_t* tq = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + MWAVES * QPW + w * QPW;
-  int32_t* stg = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + 2 * MWAVES * QPW + w * (STG + 1);
-  float* sd = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT) + 2 * MWAVES * QPW +
-                                       MWAVES * (STG + 1)) + w * MB * 32;
+  uint8_t* pk = smem + w * (NPR * PKT);  // this wave's ring
+  int32_t* wbase = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT);
+  int32_t* lcnt = wbase + w * QPW;                      // this wave's list lengths
+  int32_t* tq = wbase + MWAVES * QPW + w * QPW;         // tau'(q) = tau(q) - pc(q)
+  int32_t* stg = wbase + 2 * MWAVES * QPW + w * (STG + 1);  // hit staging (+1 spare)
+  float* sd = reinterpret_cast<float*>(wbase + 2 * MWAVES * QPW + MWAVES * (STG + 1)) + w * MB * 32;
   const int l = lane_id();
   const int h = l >> 5, ri = l & 31;
   const int nb = gridDim.x, b = blockIdx.x;
@@ -894,6 +770,8 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
   const int nblk = 2 * ntiles;  // 32-row n-blocks
 
   // LDS-DMA of packed tile t: 8 pieces of 64 x 16 B (the K1m swizzle), the last partial tile clamped
+  // to the chunk's last row.  (Source and destination of the builtin through locals: a compound
+  // expression in its arguments makes the host-side compile silently drop the kernel's launch stub.)
   uint32_t doff[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -907,16 +785,19 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
     if (tr0 + RT <= row1) {
       const uint8_t* base = codes + tr0 * 128;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + i * 1024), 16,
-                                         0, VRQ_K1R_AUX);
+      for (int i = 0; i < 8; ++i) {
+        const uint8_t* src = base + doff[i];
+        uint8_t* dst = buf + i * 1024;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, K1R_AUX);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         int64_t row = tr0 + (doff[i] >> 7);
         row = row < row1 ? row : row1 - 1;
-        __builtin_amdgcn_global_load_lds(codes + row * 128 + (doff[i] & 127),
-                                         (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        const uint8_t* src = codes + row * 128 + (doff[i] & 127);
+        uint8_t* dst = buf + i * 1024;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
     }
   };
@@ -948,29 +829,35 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
   for (int m = 0; m < MB; ++m)
     if (l < 32) {
       const int g = l & 15, hh = l >> 4;
-      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];  // (K1r: untagged)
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
     }
   const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), stg0 = lds_addr(stg);
   const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
-  auto load_seed = [&](v16f& a, int m) __attribute__((always_inline)) {
+  // the accumulator seeds tau'/2 of M-block m: this lane's 16 values.  SYNC: retired here, before
+  // the four pieces are joined; otherwise retired by the caller's wait, which names `a`
+  auto load_seed = [&](v16f& a, int m, auto SYNC) __attribute__((always_inline)) {
     v4i p0, p1, p2, p3;
     lds_read128(p0, sd0 + (uint32_t)(m * 128));
     lds_read128(p1, sd0 + (uint32_t)(m * 128 + 16));
     lds_read128(p2, sd0 + (uint32_t)(m * 128 + 32));
     lds_read128(p3, sd0 + (uint32_t)(m * 128 + 48));
+    if constexpr (decltype(SYNC)::value)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
     const v16i x = __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7),
                                            __builtin_shufflevector(p2, p3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4,
                                            5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
     a = __builtin_bit_cast(v16f, x);
   };
+  // SEEDREG: the seeds stay in registers for the whole kernel and every n-block's first MFMA takes
+  // them as its C operand; otherwise (MB = 4) they are re-read from LDS into the accumulators of
+  // the other parity while this n-block's MFMAs run
+  v16f seedv[SEEDREG ? MB : 1];
   v16f acc[2][MB];
-  if constexpr (!DENSE)
-    static_for<0, MB>([&](auto M) {
-      constexpr int m = decltype(M)::value;
-      load_seed(acc[0][m], m);
-      load_seed(acc[1][m], m);
-    });
-  // this lane's 64 bytes of row (32 * (blk & 1) + ri) of the packed tile in ring slot `sl`
+  if constexpr (!DENSE) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) load_seed(SEEDREG ? seedv[SEEDREG ? m : 0] : acc[0][m], m, std::true_type{});
+  }
+  // this lane's 64 bytes of row (32 * (blk & 1) + ri) of the packed tile of n-block blk
   auto read_rows = [&](v4i (&d)[4], int blk) __attribute__((always_inline)) {
     const int r = 32 * (blk & 1) + ri;
     const uint32_t base = pk0 + (uint32_t)(((blk >> 1) % NPR) * PKT);
@@ -985,9 +872,9 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
   };
   static_assert(NPR - 1 <= 2, "wait_tiles covers up to 2 tiles in flight");
   wait_tiles((ntiles < NPR ? ntiles : NPR) - 1);  // tile 0 landed
-  v4i cur[4], nxt[4];
-  read_rows(cur, 0);
-  wait_lgkm0();
+  v4i rb[2][4];                                   // packed rows of the n-blocks of parity 0 / 1
+  read_rows(rb[0], 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[0][0]), "+v"(rb[0][1]), "+v"(rb[0][2]), "+v"(rb[0][3])::"memory");
 
   const int64_t qstride = (int64_t)nchunks * capc;
   uint64_t* const cbase = cand + (int64_t)chunk * capc;  // + q * qstride + pos
@@ -1034,12 +921,9 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
   // DENSE: the 16 values v = dist - pc(q) of M-block m of an n-block (local row lr of the chunk) fold
   // into this lane's running minima (as K1m's)
   DenseMin<DENSE, MB> dmin;
-  auto block_dense = [&](const v16f& a, int m, int pc, int lr) __attribute__((always_inline)) {
-    dmin.fold(a, m, pc, lr < nrows);
-  };
   // ---- main loop over n-blocks; k-step s runs the MB MFMAs of n-block blk on the unpacked dword
-  // s of `cur`, while the previous n-block's epilogue, this block's row popcount and the next
-  // block's packed reads fill the MFMA gaps ----
+  // s of rb[par], while the previous n-block's epilogue, this block's row popcount and the next
+  // block's packed reads (into rb[par ^ 1]) fill the MFMA gaps ----
   int pcs = 0;       // running row popcount of this n-block (this lane's half)
   int pprev = 0;     // the previous n-block's row popcount (whole row)
   int hpb = 0x7fffffff;
@@ -1047,8 +931,8 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
 #pragma unroll
   for (int m = 0; m < MB; ++m) hitm[m] = 0;
   auto nblock = [&](auto PAR, int blk) __attribute__((always_inline)) {
-    constexpr int par = decltype(PAR)::value;  // blk & 1 (n-blocks run in pairs: static accumulator indices)
-    // the next n-block's tile: its DMA landed (tile boundary), and the ring slot of tile t+NPR-1 ...
+    constexpr int par = decltype(PAR)::value;  // blk & 1 (n-blocks run in pairs: static register sets)
+    // the next n-block's tile: its DMA landed (tile boundary)
     if (par == 1 && blk + 1 < nblk) {
       const int t1 = (blk + 1) >> 1;  // tile about to be read
       const int last = t1 + NPR - 1 < ntiles ? t1 + NPR - 1 : ntiles - 1;  // last tile issued so far
@@ -1057,12 +941,16 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
     const int lr = blk * 32 + ri;
     static_for<0, KS>([&](auto S) {
       constexpr int s = decltype(S)::value;
-      const uint32_t wd = (uint32_t)cur[s >> 2][s & 3];
+      const uint32_t wd = (uint32_t)rb[par][s >> 2][s & 3];
       const v4i bfrag = unpack_row32(wd);
       static_for<0, MB>([&](auto M) {
         constexpr int m = decltype(M)::value;
-        if constexpr (s == 0 && !DENSE) asm volatile("" : "+v"(acc[par][m]));
-        acc[par][m] = mfma_fp4(A[m][s], bfrag, (s == 0 && DENSE) ? v16f{} : acc[par][m]);
+        if constexpr (s == 0 && DENSE)
+          acc[par][m] = mfma_fp4(A[m][s], bfrag, v16f{});
+        else if constexpr (s == 0 && SEEDREG)
+          acc[par][m] = mfma_fp4(A[m][s], bfrag, seedv[SEEDREG ? m : 0]);
+        else
+          acc[par][m] = mfma_fp4(A[m][s], bfrag, acc[par][m]);
         asm volatile("" : "+v"(acc[par][m]));
       });
       VRQ_SCHED_FENCE();
@@ -1072,7 +960,7 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
         pcs += __popc(wd);
       // epilogue of the previous n-block: tests (s = 1 .. MB), branch (s = MB + 1), re-seeds
       if constexpr (DENSE && s >= 1 && s < 1 + MB) {
-        if (blk > 0) block_dense(acc[par ^ 1][s - 1], s - 1, pprev, lr - 32);
+        if (blk > 0) dmin.fold(acc[par ^ 1][s - 1], s - 1, pprev, lr - 32 < nrows);
       }
       if constexpr (!DENSE && s >= 1 && s < 1 + MB) {
         constexpr int m = s - 1;
@@ -1097,22 +985,29 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
           if (nst) flush_all(row0 + (int64_t)(blk - 1) * 32);
         }
       }
-      if constexpr (!DENSE && s >= MB + 2 && s < 2 * MB + 2) load_seed(acc[par ^ 1][s - MB - 2], s - MB - 2);
+      if constexpr (!DENSE && !SEEDREG && s >= MB + 2 && s < 2 * MB + 2)
+        load_seed(acc[par ^ 1][s - MB - 2], s - MB - 2, std::false_type{});
       // the next n-block's packed data
       if constexpr (s == 8)
-        if (blk + 1 < nblk) read_rows(nxt, blk + 1);
+        if (blk + 1 < nblk) read_rows(rb[par ^ 1], blk + 1);
       VRQ_SCHED_FENCE();
     });
     // row popcount of this n-block (both halves) and its threshold for the next n-block's tests
     pprev = pcs + __shfl_xor(pcs, 32, 64);
     hpb = __float_as_int(0.5f * (float)(lr < nrows ? pprev : 0x40000000));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3])::"memory");
-    // tile t = blk >> 1 consumed once its second n-block's rows are in registers (nxt, read during
-    // the first n-block and complete here): refill its ring slot with the DMA of tile t + NPR, an
-    // n-block earlier than after the second n-block
+    // retire the reads of this n-block: every destination register is an operand of the wait
+    if constexpr (!DENSE && !SEEDREG) {
+      static_assert(MB == 4, "re-seeded instance");
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(rb[par ^ 1][0]), "+v"(rb[par ^ 1][1]), "+v"(rb[par ^ 1][2]), "+v"(rb[par ^ 1][3]),
+                     "+v"(acc[par ^ 1][0]), "+v"(acc[par ^ 1][1]), "+v"(acc[par ^ 1][2]), "+v"(acc[par ^ 1][3])::"memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(rb[par ^ 1][0]), "+v"(rb[par ^ 1][1]), "+v"(rb[par ^ 1][2]), "+v"(rb[par ^ 1][3])::"memory");
+    }
+    // tile t = blk >> 1 consumed once its second n-block's rows are in registers (rb[1], read during
+    // the first n-block and retired here): refill its ring slot with the DMA of tile t + NPR
     if (par == 0 && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
   };
   for (int blk = 0; blk < nblk; blk += 2) {  // nblk is even
     nblock(std::integral_constant<int, 0>{}, blk);
@@ -1123,7 +1018,7 @@ __global__ __launch_bounds__(MWAVES * 64, k1r_occ<MB>()) void hamming_mfma_rows_
     constexpr int par = 1;
     const int lr = (nblk - 1) * 32 + ri;
     if constexpr (DENSE) {
-      static_for<0, MB>([&](auto M) { block_dense(acc[par][decltype(M)::value], decltype(M)::value, pprev, lr); });
+      static_for<0, MB>([&](auto M) { dmin.fold(acc[par][decltype(M)::value], decltype(M)::value, pprev, lr < nrows); });
     } else {
       const int pc = lr < nrows ? pprev : 0x40000000;
       const float hp = 0.5f * (float)pc;
@@ -1484,7 +1379,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
     p->nqb = 1;
-    rows_occ = p->mb == 1 ? k1r_occ<1>() : p->mb == 2 ? k1r_occ<2>() : k1r_occ<4>();
+    rows_occ = p->mb == 1 ? RowsShape<1>::OCC : p->mb == 2 ? RowsShape<2>::OCC : RowsShape<4>::OCC;
   }
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
@@ -1518,7 +1413,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->sample = tiles * RT;
   p->dvcols = nsc * 32;  // the dense pass writes 32 lane minima per (query, sample chunk)
   S = p->sample;
-  // thresholded pass over all n rows (K1r: one chunk per wave, 1024 waves per workgroup slot of a CU)
+  // thresholded pass over all n rows (K1r: one chunk per wave, MWAVES waves per workgroup slot of a CU)
   int64_t want = p->rows ? 256 * MWAVES * rows_occ : 256 / p->nqb;
   if (want < 1) want = 1;
   int64_t cr = (n + want - 1) / want;
@@ -1575,7 +1470,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
       hipLaunchKernelGGL(kern2, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
                          crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
   };
-  // K1r launches: the MB = 1 / 2 / 4 instance, one workgroup per 4 chunks
+  // K1r launches: the MB = 1 / 2 / 4 instance, one workgroup per MWAVES chunks
   auto rows_pass = [&](auto k1, auto k2, auto k4, const int32_t* tau, const int32_t* rr, const int32_t* qf,
                        int nch, int64_t crows, int64_t cstride, int64_t tstride, uint16_t* d, int64_t dstride) {
     const dim3 g((unsigned)((nch + MWAVES - 1) / MWAVES)), blk(MWAVES * 64);

@@ -633,6 +633,28 @@ int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, 
   return VRQ_SCAN_KIND_VALU;
 }
 
+int vrq_scan_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* info) {
+  if (!info || n < 1 || nq < 1 || K < 1) return VRQ_EINVAL;
+  if (dim != DIM || K > KMAX) return VRQ_EUNSUPPORTED;
+  if (!mfma_use(n, nq, K, flags)) return VRQ_EUNSUPPORTED;
+  MfmaPlan p;
+  const int rc = mfma_plan(n, nq, K, &p);
+  if (rc != VRQ_OK) return rc;
+  info[0] = p.rows;
+  info[1] = p.mb;
+  info[2] = p.chunk_rows;
+  info[3] = p.nchunks;
+  info[4] = p.capc;
+  info[5] = (int64_t)p.off_cand;
+  info[6] = (int64_t)p.off_cnt;
+  info[7] = (int64_t)p.off_tau;
+  info[8] = p.sample;
+  info[9] = p.j;
+  info[10] = (int64_t)p.off_suffix;
+  info[11] = (int64_t)p.bytes;
+  return VRQ_OK;
+}
+
 int vrq_merge_shards(int32_t nshards, int32_t nq, int32_t K, const int32_t* counts, const int64_t* rows,
                      const int32_t* dist, const double* s2, const double* s3, int32_t k, int32_t K3,
                      int32_t* out_count, int64_t* out_rows, int32_t* out_dist, double* out_binary,
