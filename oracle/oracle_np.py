@@ -161,8 +161,11 @@ def three_phase_search(index: IndexBinaryIDMap2, doc_int8: dict, doc_text: dict,
 
 def three_phase_batch(codes: np.ndarray, int8: np.ndarray, ids: np.ndarray,
                       qf: np.ndarray, qb: np.ndarray, k: int = 10,
-                      binary_oversample: int = 10, int8_oversample: int = 3):
+                      binary_oversample: int = 10, int8_oversample: int = 3, phase1=None):
     """Array form of ``three_phase_search`` for many queries (oracle for the GPU path).
+
+    ``phase1`` = (D, I) of the Phase-I top-``k * binary_oversample`` when already computed (e.g. by
+    the C restatement of hammings_knn_hc for a large corpus); otherwise ``binary_flat_search``.
 
     Rows are internal indices (insertion order); ``ids`` is the id map.
     Returns per query a dict of arrays: ``row`` (internal index), ``doc_id``,
@@ -178,7 +181,7 @@ def three_phase_batch(codes: np.ndarray, int8: np.ndarray, ids: np.ndarray,
     if n == 0:
         return [None] * qf.shape[0]
     binary_k = min(k * binary_oversample, n)
-    D, I = binary_flat_search(codes, qb, binary_k)
+    D, I = binary_flat_search(codes, qb, binary_k) if phase1 is None else phase1
     norms = int8_row_norms(int8)
     for q in range(qf.shape[0]):
         rows = I[q][I[q] >= 0]

@@ -4,6 +4,10 @@
   north_star target "top-10 ids identical to the CPU reference at N = 100M"): the matrix-core
   small-batch scan (K1r) at nq = 1, 8 and 64, K = 100, against the C restatement of FAISS
   hammings_knn_hc over every row.  Every (dist, row) of the top-K must be identical.
+* Config 2 -- the 3-phase search over 1M rows with the full nq = 1024 batch, i.e. the MB = 4 instance
+  of the shared-tile matrix-core scan (K1m) the config-2 bench runs: 32 sampled queries against the
+  FAISS restatement (Phase I, every (dist, row) of the top-K) and the reference Phases II/III
+  (CohereEnhancedVectorDB.py:267-322).
 * Config 5 -- exhaustive Phase-II / Phase-III top-k over 10M x 1024 rows, nq = 1024 (four 256-query
   blocks per chunk, the retry path at scale), with the exact fallback OFF (VRQ_GEMM_NO_FALLBACK):
   a sample of 16 queries against the reference scores of EVERY row, computed in float64 on the GPU
@@ -115,3 +119,40 @@ def test_config5_full_shape_vs_exact_scores(dev):
         del S
     del sh, codes, x8, norms
     torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(300)
+def test_config2_1m_batch_1024_vs_reference(dev, oracle_lib):
+    from oracle import oracle_np as O
+    from tests.test_gpu_parity import MAX_TIE_FRAC, _certify
+    from vectorragquantization_amd import _native as N
+    from vectorragquantization_amd import synth
+    from vectorragquantization_amd.enhanced import search3
+    n, nq, k, K, K3 = 1_000_000, 1024, 10, 100, 30
+    lib = N.load()
+    info = np.zeros(12, np.int64)
+    N.check(lib.vrq_scan_plan(n, 1024, nq, K, 0, info.ctypes.data), "plan")
+    assert int(info[0]) == 0 and int(info[1]) == 4, info[:2]  # K1m, 4 M-blocks per wave
+    sh = synth.make_corpus(n, device=dev)
+    codes, x8, norms = sh["codes"], sh["x8"], sh["norms"]
+    qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    cnt, rows, dist, s2, s3 = (t.cpu().numpy() for t in search3(codes, x8, norms, qf, qb, k, K, K3, 0))
+    c1, r1, d1, _, _ = (t.cpu().numpy() for t in search3(codes, x8, norms, qf, qb, k, K, K3,
+                                                          N.VRQ_SEARCH_PHASE1_ONLY))
+    torch.cuda.synchronize()
+    sample = np.arange(3, nq, nq // 32)[:32]                 # spread over the four 256-query blocks
+    codes_h, x8_h = codes.cpu().numpy(), x8.cpu().numpy()
+    qf_h, qb_h = qf.cpu().numpy()[sample], qb.cpu().numpy()[sample]
+    D, I = oracle_knn(oracle_lib, codes_h, qb_h, K, threads=16)
+    assert (c1[sample] == K).all()
+    assert np.array_equal(d1[sample], D) and np.array_equal(r1[sample], I)
+    ref = O.three_phase_batch(codes_h, x8_h, np.arange(n, dtype=np.int64), qf_h, qb_h, k, K // k, K3 // k,
+                              phase1=(D, I))
+    ties = 0
+    for j, q in enumerate(sample.tolist()):
+        assert int(cnt[q]) == k
+        same = _certify(qf_h[j], qb_h[j], codes_h, x8_h, rows[q], dist[q], s2[q], s3[q], ref[j]["row"])
+        if same:
+            assert np.array_equal(s2[q], ref[j]["binary"])
+        ties += not same
+    assert ties <= MAX_TIE_FRAC * len(sample) + 1

@@ -113,11 +113,14 @@ def test_gemm_topk_edge_cases(dev):
     _check("binary", qf, k, cnt, rows, sc, codes=codes[:3])
 
 
-def test_gemm_topk_all_identical_rows(dev):
+@pytest.mark.parametrize("nq", [3, 300])
+def test_gemm_topk_all_identical_rows(dev, nq):
     """Every row identical: all scores tie, the sampled threshold admits every row -> list overflow
-    -> exact fallback, which must return rows 0..k-1."""
+    -> exact fallback, which must return rows 0..k-1.  nq = 300 floods the thresholded pass with a
+    whole 256-query block plus a partial one: every (query, row) of every tile is a hit, so the hit
+    stage, the per-chunk list counters and the list appends all run at their capacity bounds."""
     rng = np.random.default_rng(9)
-    n, nq, k = 50_000, 3, 10
+    n, k = 50_000, 10
     F = np.repeat(_corpus(rng, 1), n, axis=0)
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = _queries(rng, _corpus(rng, 100), nq)

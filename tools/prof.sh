@@ -6,7 +6,7 @@
 # counter block per pass, MI355X_MICROARCH.md), condensed by tools/summarize_profile.py into
 # gpurun_out/$TAG/<config>_nq<nq>/summary.json.  tools/collect_profiles.py copies them into profiles/.
 # Each GPU step is time-limited; the chain stops at the first failure.
-#   RUNS="c3:1 c3:8 c3:64 c2:1024 c4:1024 c5:1024"  TAG=name  PMC=1|0  SQ=0|1  STEPS=20 WARMUP=3
+#   RUNS="c3:1 c3:8 c3:64 c2:1024 c4:1024 c5:1024"  TAG=name  PMC=1|0  SQ=0|1  CLK=0|1  STEPS=20 WARMUP=3
 #   BARGS="extra bench args"
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -25,10 +25,13 @@ for run in ${RUNS:-c3:8}; do
   if [ "${SQ:-0}" = "1" ]; then  # one SQ pass (<= 8 SQ counters): wait / busy / MFMA-busy fractions
     timeout -k 10 ${PT:-400} rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA -d $OUT/pmc_sq -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 $B > $OUT/pmc_sq.log 2>&1 || { echo SQ_FAIL $run; tail -20 $OUT/pmc_sq.log; exit 1; }
   fi
+  if [ "${CLK:-0}" = "1" ]; then  # effective clock and matrix-core busy fraction (MI355X_MICROARCH.md DVFS notes)
+    timeout -k 10 ${PT:-400} rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES -d $OUT/pmc_clk -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 $B > $OUT/pmc_clk.log 2>&1 || { echo CLK_FAIL $run; tail -20 $OUT/pmc_clk.log; exit 1; }
+  fi
   python3 tools/summarize_profile.py $OUT $OUT/summary.json ${CFG}_nq${NQ} > /dev/null
   # keep the condensed results only (the raw per-dispatch CSVs of a 100M-row run exceed gpurun's 64 MiB)
   cp "$(find $OUT/trace -name '*kernel_stats.csv' | head -1)" $OUT/kernel_stats.csv
-  rm -rf $OUT/trace $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_sq
+  rm -rf $OUT/trace $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_sq $OUT/pmc_clk
   echo "== $run"; cat $OUT/dispatch.txt
   python3 -c "import json; print('   events', json.load(open('$OUT/bench_trace.json'))['phase_ms'])"
 done

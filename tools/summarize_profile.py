@@ -60,7 +60,7 @@ def main(src, dst, tag):
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         out["kernel_stats"] = [r for r in csv.DictReader(open(stats[0]))]
-    for name in ("pmc_sq", "pmc_mfma", "pmc_v", "pmc_fetch", "pmc_write"):
+    for name in ("pmc_sq", "pmc_mfma", "pmc_v", "pmc_fetch", "pmc_write", "pmc_clk"):
         f = glob.glob(os.path.join(src, name, "**", "*counter_collection.csv"), recursive=True)
         if f:
             out[name] = pmc(f[0])
@@ -73,6 +73,20 @@ def main(src, dst, tag):
         except KeyError:
             continue
         out["bytes_per_launch"][k] = fetch + write
+    # effective shader clock under load (GRBM_GUI_ACTIVE is the sum over the 8 XCDs) and the
+    # matrix-core busy fraction (SQ_VALU_MFMA_BUSY_CYCLES sums MFMA cycles over all 1024 SIMDs)
+    avg_ns = {}
+    for r in out.get("kernel_stats", []):
+        avg_ns.setdefault(short(r.get("Name", r.get("KernelName", ""))), float(r.get("AverageNs", 0) or 0))
+    out["clock"] = {}
+    for k, c in out.get("pmc_clk", {}).items():
+        cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        if cyc <= 0:
+            continue
+        d = {"cycles_per_xcd": cyc, "mfma_busy_frac": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * cyc)}
+        if avg_ns.get(k):
+            d["eff_clock_ghz"] = cyc / avg_ns[k]
+        out["clock"][k] = d
     if "hamming_scan_kernel" in out["bytes_per_launch"]:
         out["scan_bytes_per_launch"] = out["bytes_per_launch"]["hamming_scan_kernel"]
     json.dump(out, open(dst, "w"), indent=1)

@@ -545,15 +545,15 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
           if constexpr (k == 0) {
             e0 = max(max(bb[0], bb[1]), bb[2]);
             e1 = max(max(bb[3], bb[4]), bb[5]);
-            asm volatile("" : "+v"(e0), "+v"(e1));
+            asm volatile("" ::"v"(e0), "v"(e1));
           } else if constexpr (k == 1) {
             e2 = max(max(bb[6], bb[7]), bb[8]);
             e3 = max(max(bb[9], bb[10]), bb[11]);
-            asm volatile("" : "+v"(e2), "+v"(e3));
+            asm volatile("" ::"v"(e2), "v"(e3));
           } else if constexpr (k == 2) {
             e4 = max(max(bb[12], bb[13]), bb[14]);
             f0 = max(max(e0, e1), e2);
-            asm volatile("" : "+v"(e4), "+v"(f0));
+            asm volatile("" ::"v"(e4), "v"(f0));
           } else {
             hitm[tm] = __ballot(max(max(e3, e4), max(bb[15], f0)) > hpb);
           }
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             u0 = wv & 0x11111111u;
             u1 = wv & 0x22222222u;
             u2 = wv & 0x44444444u;
-            asm volatile("" : "+v"(u0), "+v"(u1), "+v"(u2));
+            asm volatile("" ::"v"(u0), "v"(u1), "v"(u2));
           } else {
             v4i r;
             r.x = (int)u0;
@@ -586,14 +586,14 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
         if constexpr (gi == 28) {  // row popcounts of tile t+2
           if constexpr (k == 0) {
             pc0 = __popc(pa.x) + __popc(pa.y) + __popc(pa.z) + __popc(pa.w);
-            asm volatile("" : "+v"(pc0));
+            asm volatile("" ::"v"(pc0));
           } else if constexpr (k == 1) {
             pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
-            asm volatile("" : "+v"(pc1));
+            asm volatile("" ::"v"(pc1));
           } else if constexpr (k == 2) {
             pc0 = pc0 + pc1;
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-            asm volatile("" : "+v"(pc0));
+            asm volatile("" ::"v"(pc0));
           } else {
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
             if ((l & 3) == 0) lds_write32(pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4 + pr * 4), pc0);
