@@ -448,25 +448,35 @@ def _round_key(path):
     return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, 0)
 
 
+# the K1r thresholded pass: hamming_mfma_rows_kernel<0, MB> (MB 1, 4) or its lean MB = 2 form
+K1R_MAIN = ("hamming_mfma_rows_kernel<0", "hamming_mfma_rows_lean_kernel<0")
+
+
+def _kname(kern):
+    """Display / profile-summary name of a kernel spec (a name prefix or a tuple of them)."""
+    return (kern if isinstance(kern, str) else kern[0]).split("<")[0]
+
+
 def rocprof_avg_ms(tag, kernel):
     """rocprofv3 duration (ms) of `kernel` for this workload tag from the newest committed summary:
     profiles/r*_<tag>_dispatch.json (tools/trace_dispatches.py: the mean over the launches after the
     bench's untimed warm-up steps, i.e. the launches the HIP events time) or else the --stats average of
     profiles/r*_<tag>_kernel_stats.csv (every launch).  Returns (ms, source, what) or None."""
     import csv
+    kernels = (kernel,) if isinstance(kernel, str) else tuple(kernel)  # name substrings, any matches
     disp = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_dispatch.json")), key=_round_key)
     stats = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{tag}_kernel_stats.csv")), key=_round_key)
     try:
         if disp and (not stats or _round_key(disp[-1]) >= _round_key(stats[-1])):
             d = json.load(open(disp[-1]))
             for name, v in d["kernels"].items():
-                if kernel in name:
+                if any(k in name for k in kernels):
                     return (v["mean_after_warmup_ms"], os.path.relpath(disp[-1], HERE),
                             f"rocprofv3 --kernel-trace: mean of the {v['n_after_warmup']} launches after "
                             f"{d['warmup']} warm-up step(s), from the same bench command")
         if stats:
             for row in csv.DictReader(open(stats[-1])):
-                if kernel in row["Name"]:
+                if any(k in row["Name"] for k in kernels):
                     return (float(row["AverageNs"]) / 1e6, os.path.relpath(stats[-1], HERE),
                             "rocprofv3 --kernel-trace --stats average over every launch (warm-up included)")
     except Exception:
@@ -838,12 +848,12 @@ def phase1_leg(dev, n, nqs, k, osb, steps, warmup, threads, cpu=True, scan="auto
         T = time.perf_counter() - t0
         st = P.stage_ms()
         mb = n * 128 + nq * 128
-        kern = "hamming_mfma_rows_kernel<0" if P.kind == N.VRQ_SCAN_KIND_MFMA and nq <= 128 else \
+        kern = K1R_MAIN if P.kind == N.VRQ_SCAN_KIND_MFMA and nq <= 128 else \
             ("hamming_mfma_kernel<0" if P.kind == N.VRQ_SCAN_KIND_MFMA else "hamming_scan_kernel")
         kms = st["matrix"] if P.kind == N.VRQ_SCAN_KIND_MFMA else st["scan"]
         ach = mb / (kms * 1e-3) / 1e9
         pt = {"nq": nq, "qps": nq * steps / T, "ms_per_step": T / steps * 1e3, "phase_ms": st,
-              "kernel": kern.rstrip("<0"), "kernel_ms": kms, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+              "kernel": _kname(kern), "kernel_ms": kms, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
               "algorithmic_bytes_per_launch": mb, "timing": f"HIP events on the library's stream, {steps} passes "
                                                             f"after {warmup} warm-up passes",
               "mfma": {"achieved": 2048.0 * nq * n / (kms * 1e-3) / 1e12, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
@@ -1087,10 +1097,10 @@ def run_3phase(a, world, rank, dev):
         rows_m = m - P.prefix_rows
         ops = 2048.0 * nq * rows_m
         ach = ops / (st["matrix"] * 1e-3) / 1e12
-        kern = "hamming_mfma_rows_kernel<0" if nq <= 128 else "hamming_mfma_kernel<0"
+        kern = K1R_MAIN if nq <= 128 else "hamming_mfma_kernel<0"
         roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
-                "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, kern.rstrip("<0")),
-                "kernel": f"{kern.rstrip('<0')} (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
+                "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, _kname(kern)),
+                "kernel": f"{_kname(kern)} (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
                 "kernel_ms": st["matrix"], "timing": "HIP events on the library's stream, this run",
                 "algorithmic_ops_per_launch": ops, "algorithmic_bytes_per_launch": rows_m * 128 + nq * 128,
                 "measured_sustained_peak": measured_mfma_peak(), "rows": rows_m,

@@ -12,9 +12,10 @@ import sys
 
 
 def short(name):
-    if "hamming_mfma_rows" in name:  # K1r, template MODE as below
+    if "hamming_mfma_rows" in name:  # K1r (and its lean MB = 2 form), template MODE as below
+        mode = name.split("_kernel<", 1)[-1][:1]
         return {"1": "hamming_mfma_rows_kernel_sample", "2": "hamming_mfma_rows_kernel_rerun"}.get(
-            name.split("hamming_mfma_rows_kernel<", 1)[-1][:1], "hamming_mfma_rows_kernel")
+            mode, "hamming_mfma_rows_kernel")
     if "hamming_mfma" in name:  # template MODE: 0 thresholded pass, 1 dense sample pass, 2 re-run
         return {"1": "hamming_mfma_kernel_sample", "2": "hamming_mfma_kernel_rerun"}.get(
             name.split("hamming_mfma_kernel<", 1)[-1][:1], "hamming_mfma_kernel")

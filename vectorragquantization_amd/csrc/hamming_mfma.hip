@@ -1037,6 +1037,264 @@ __global__ __launch_bounds__(MWAVES * 64, RowsShape<MB>::OCC) void hamming_mfma_
       if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
 }
 
+// K1r for batches of <= 64 queries (MB <= 2): the per-wave chunk scan of hamming_mfma_rows_kernel with
+// a register budget that keeps TWO waves on every SIMD at MB = 2 as well (round 4; the MB = 2
+// instance above holds 328 registers and runs one wave per SIMD, 0.58 of HBM at nq = 64):
+//   * one accumulator set per M-block: the n-block's tests run after its 16 k-steps (the first test
+//     waits for the last MFMA; the SIMD's other wave fills that gap) instead of in the next
+//     n-block's MFMA shadow, which needed a second set;
+//   * one set of packed-row registers: quad i (k-steps 4i .. 4i+3) of the NEXT n-block is read into
+//     rb[i] right after k-step 4i+3 consumed it; all four are retired by one wait after the n-block's
+//     tests (the last quad has had the tests' time to land), so no read is in flight across the loop
+//     back-edge, where the register allocator may copy a loop-carried value;
+//   * the seeds tau'/2 stay in registers (the C operand of every n-block's first MFMA).
+// A, the thresholds, the lists and the DMA ring are as in hamming_mfma_rows_kernel (ring of 2 tiles
+// per wave; tile t's slot is refilled once the last quad read from it has been retired).
+template <int MB>
+struct LeanShape {
+  static_assert(MB == 2, "lean K1r: the MB = 2 instance");
+  static constexpr int QPW = 32 * MB;
+  static constexpr int NPR = 2;
+  static constexpr int SMEM = MWAVES * (NPR * PKT + QPW * 8 + (STG + 1) * 4 + MB * 128);
+  static_assert(2 * SMEM <= 160 * 1024, "LDS budget of two workgroups per CU");
+};
+
+template <int MODE, int MB>
+__global__ __launch_bounds__(MWAVES * 64, 2) void hamming_mfma_rows_lean_kernel(
+    const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
+    const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
+    int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
+    const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
+  constexpr bool DENSE = MODE == MFMA_SAMPLE;
+  constexpr int QPW = LeanShape<MB>::QPW, NPR = LeanShape<MB>::NPR;
+  if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LeanShape<MB>::SMEM];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* pk = smem + w * (NPR * PKT);  // this wave's ring
+  int32_t* wbase = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT);
+  int32_t* lcnt = wbase + w * QPW;
+  int32_t* tq = wbase + MWAVES * QPW + w * QPW;
+  int32_t* stg = wbase + 2 * MWAVES * QPW + w * (STG + 1);
+  float* sd = reinterpret_cast<float*>(wbase + 2 * MWAVES * QPW + MWAVES * (STG + 1)) + w * MB * 32;
+  const int l = lane_id();
+  const int h = l >> 5, ri = l & 31;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3, q8 = nb >> 3, r8 = nb & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int chunk = L * MWAVES + w;
+  if (chunk >= nchunks) return;
+  const int64_t row0 = (int64_t)chunk * chunk_stride;
+  const bool strided = tile_stride != RT;
+  const int64_t row1 = strided ? n : (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  if (row0 >= row1) return;
+  const int nrows = strided ? (int)chunk_rows : (int)(row1 - row0);
+  const int ntiles = (nrows + RT - 1) / RT;
+  const int nblk = 2 * ntiles;
+
+  // LDS-DMA of packed tile t: piece i (rows 8i .. 8i+7) of the K1m swizzle puts lane l at tile byte
+  // i * 1024 + lo[i & 1] with lo[0] = (l >> 3) * 128 + ((l & 7) ^ (l >> 4)) * 16, lo[1] = lo[0] ^ 64:
+  // two per-lane offsets (the byte offset of piece i is uniform), recomputed from an opaque lane id
+  // at every issue so that no per-piece 64-bit address stays live across the loop
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    int lo_ = l;
+    asm volatile("" : "+v"(lo_));
+    const uint32_t lo0 = (uint32_t)((lo_ >> 3) * 128 + ((lo_ & 7) ^ (lo_ >> 4)) * 16);
+    uint8_t* buf = pk + (t % NPR) * PKT;
+    const int64_t tr0 = row0 + (int64_t)t * tile_stride;
+    const bool whole = tr0 + RT <= row1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t off = lo0 ^ (uint32_t)((i & 1) * 64);
+      int64_t row = tr0 + 8 * i + (int64_t)(off >> 7);
+      if (!whole) row = row < row1 ? row : row1 - 1;  // the last partial tile: clamp to the chunk's last row
+      const uint8_t* src = codes + row * 128 + (off & 127);
+      uint8_t* dst = buf + i * 1024;
+      if (whole)
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, K1R_AUX);
+      else
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  for (int t = 0; t < NPR && t < ntiles; ++t) issue(t);
+
+  v4i A[MB][KS];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int q = 32 * m + ri;
+    const bool qok = q < nq && (!rerun || rerun[q]);
+    const uint32_t* qp = reinterpret_cast<const uint32_t*>(queries + (int64_t)(qok ? q : 0) * 128);
+    int pc = 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint32_t wd = qok ? qp[16 * h + s] : 0u;
+      pc += __popc(wd);
+      A[m][s] = unpack_query32(wd);
+    }
+    pc += __shfl_xor(pc, 32, 64);
+    if (h == 0) tq[q] = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;
+  }
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(A[m][s]));
+  for (int i = l; i < QPW; i += 64) lcnt[i] = 0;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+    if (l < 32) {
+      const int g = l & 15, hh = l >> 4;
+      sd[m * 32 + l] = 0.5f * (float)tq[32 * m + (g & 3) + 8 * (g >> 2) + 4 * hh];
+    }
+  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(h * 64), stg0 = lds_addr(stg);
+  const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
+  v16f seedv[MB];
+  if constexpr (!DENSE) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      v4i p0, p1, p2, p3;
+      lds_read128(p0, sd0 + (uint32_t)(m * 128));
+      lds_read128(p1, sd0 + (uint32_t)(m * 128 + 16));
+      lds_read128(p2, sd0 + (uint32_t)(m * 128 + 32));
+      lds_read128(p3, sd0 + (uint32_t)(m * 128 + 48));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
+      const v16i x = __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                             __builtin_shufflevector(p2, p3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3,
+                                             4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      seedv[m] = __builtin_bit_cast(v16f, x);
+    }
+  }
+  // quad i of this lane's 64 bytes of row (32 * (blk & 1) + ri) of n-block blk's packed tile
+  auto read_quad = [&](v4i& d, int i, int blk) __attribute__((always_inline)) {
+    const int r = 32 * (blk & 1) + ri;
+    lds_read128_inplace(d, pk0 + (uint32_t)(((blk >> 1) % NPR) * PKT) + (uint32_t)(pk_slot(r, 4 * h + i) * 16));
+  };
+  auto wait_tiles = [&](int k) __attribute__((always_inline)) {
+    if (k <= 0) wait_vm<0>();
+    else wait_vm<8>();
+  };
+  static_assert(NPR - 1 <= 1, "wait_tiles covers one tile in flight");
+  wait_tiles((ntiles < NPR ? ntiles : NPR) - 1);  // tile 0 landed
+  v4i rb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) read_quad(rb[i], i, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[0]), "+v"(rb[1]), "+v"(rb[2]), "+v"(rb[3])::"memory");
+
+  const int64_t qstride = (int64_t)nchunks * capc;
+  uint64_t* const cbase = cand + (int64_t)chunk * capc;
+  int nst = 0;
+  auto flush_all = [&](int64_t base_row) __attribute__((always_inline)) {
+    if (nst > STG) {
+      for (int i = l; i < QPW; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
+      nst = STG;
+    }
+    for (int i0 = 0; i0 < nst; i0 += 64) {
+      const int i = i0 + l;
+      int e = 0, pos = 0;
+      if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+      const int ql = (e >> ENT_Q_SHIFT) & 127;
+      if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+      if (i < nst && pos < capc)
+        cbase[(int64_t)ql * qstride + pos] =
+            ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) | (uint64_t)(base_row + (e & 127));
+    }
+    nst = 0;
+  };
+  auto block_hits = [&](const v16f& a, int m, int pc, float hp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const uint64_t mask = __ballot(a[g] > hp);
+      if (mask) {
+        if ((mask >> l) & 1) {
+          const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+          int lo = l;
+          asm volatile("" : "+v"(lo));
+          const int ql = 32 * m + (g & 3) + 8 * (g >> 2) + 4 * (lo >> 5);
+          const int v = pc - (int)(2.0f * a[g]);
+          const int pos = nst + below < STG ? nst + below : STG;
+          lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (lo & 31));
+        }
+        nst += __popcll(mask);
+      }
+    }
+  };
+  DenseMin<DENSE, MB> dmin;
+  v16f acc[MB];
+  for (int blk = 0; blk < nblk; ++blk) {
+    // entering the second n-block of tile t: the next n-block's quads (read from k-step 3 on) come from
+    // tile t + 1, which must have landed (the wave's own DMA: no barrier)
+    if ((blk & 1) && blk + 1 < nblk) {
+      const int t1 = (blk + 1) >> 1;
+      const int last = t1 + NPR - 1 < ntiles ? t1 + NPR - 1 : ntiles - 1;  // last tile issued so far
+      wait_tiles(last - t1);
+    }
+    const int nx = blk + 1 < nblk ? blk + 1 : blk;
+    int pcs = 0;
+    static_for<0, KS>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      const uint32_t wd = (uint32_t)rb[s >> 2][s & 3];
+      const v4i bfrag = unpack_row32(wd);
+      static_for<0, MB>([&](auto M) {
+        constexpr int m = decltype(M)::value;
+        if constexpr (s == 0 && DENSE)
+          acc[m] = mfma_fp4(A[m][s], bfrag, v16f{});
+        else if constexpr (s == 0)
+          acc[m] = mfma_fp4(A[m][s], bfrag, seedv[m]);
+        else
+          acc[m] = mfma_fp4(A[m][s], bfrag, acc[m]);
+        asm volatile("" : "+v"(acc[m]));
+      });
+      VRQ_SCHED_FENCE();
+      pcs += __popc(wd);
+      // (unconditional: the last n-block re-reads its own rows, unused -- a read under a branch would
+      // merge two register sets at the join, by copies the allocator may place before the wait)
+      if constexpr ((s & 3) == 3) read_quad(rb[s >> 2], s >> 2, nx);
+      VRQ_SCHED_FENCE();
+    });
+    // epilogue of this n-block (its rows: local lr)
+    const auto pp = __builtin_amdgcn_permlane32_swap((uint32_t)pcs, (uint32_t)pcs, false, false);
+    const int prow = (int)(pp[0] + pp[1]);  // row popcount (both lane halves)
+    const int lr = blk * 32 + ri;
+    if constexpr (DENSE) {
+      static_for<0, MB>([&](auto M) { dmin.fold(acc[decltype(M)::value], decltype(M)::value, prow, lr < nrows); });
+    } else {
+      const int pc = lr < nrows ? prow : 0x40000000;
+      const float hp = 0.5f * (float)pc;
+      const int hpb = __float_as_int(hp);
+      uint64_t hitm[MB];
+      uint64_t any = 0;
+      static_for<0, MB>([&](auto M) {
+        constexpr int m = decltype(M)::value;
+        const v16i bb = __builtin_bit_cast(v16i, acc[m]);
+        const int x0 = max(max(bb[0], bb[1]), bb[2]), x1 = max(max(bb[3], bb[4]), bb[5]);
+        const int x2 = max(max(bb[6], bb[7]), bb[8]), x3 = max(max(bb[9], bb[10]), bb[11]);
+        const int x4 = max(max(bb[12], bb[13]), bb[14]);
+        hitm[m] = __ballot(max(max(max(x0, x1), x2), max(max(x3, x4), bb[15])) > hpb);
+        any |= hitm[m];
+      });
+      if (any) {  // rare
+        static_for<0, MB>([&](auto M) {
+          constexpr int m = decltype(M)::value;
+          if (hitm[m]) block_hits(acc[m], m, pc, hp);
+        });
+        if (nst) flush_all(row0 + (int64_t)blk * 32);
+      }
+    }
+    // the next n-block's rows landed (every destination named)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[0]), "+v"(rb[1]), "+v"(rb[2]), "+v"(rb[3])::"memory");
+    // after n-block 2t every read from tile t is retired: its ring slot takes the DMA of tile t + NPR
+    // (issued before the wait for tile t + 1 at the top of n-block 2t+1, which counts it)
+    if (!(blk & 1) && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
+  }
+  wait_lgkm0();
+  if constexpr (DENSE)
+    dmin.out(dv, dv_stride, (int64_t)chunk * 32 + ri, 0, h, nq);
+  else
+    for (int i = l; i < QPW; i += 64)
+      if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
+}
+
 // Thresholds from the dense sample (S rows spread over the corpus, every distance exact):
 //   tau_p(q) = d_(K) + 1, accept dist <= the K-th smallest sample distance: the sample rows alone
 //              put >= K corpus rows under it, so the candidates always hold the exact top-K
@@ -1379,7 +1637,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
     p->nqb = 1;
-    rows_occ = p->mb == 1 ? RowsShape<1>::OCC : p->mb == 2 ? RowsShape<2>::OCC : RowsShape<4>::OCC;
+    rows_occ = p->mb == 1 ? RowsShape<1>::OCC : p->mb == 2 ? 2 /* lean */ : RowsShape<4>::OCC;
   }
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
@@ -1485,7 +1743,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                          qf, d, dstride);
   };
   if ((st & VRQ_SCAN_STAGE_PREFIX) && p.rows_sample) {  // dense sample pass (K1r) + per-query thresholds
-    rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>,
+    rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_lean_kernel<MFMA_SAMPLE, 2>,
               hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
               p.sample_stride, p.sample_tile_stride, dv, p.dvcols);
     VRQ_LAUNCH_CHECK();
@@ -1503,7 +1761,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_MATRIX) && p.rows) {
-    rows_pass(hamming_mfma_rows_kernel<MFMA_MAIN, 1>, hamming_mfma_rows_kernel<MFMA_MAIN, 2>,
+    rows_pass(hamming_mfma_rows_kernel<MFMA_MAIN, 1>, hamming_mfma_rows_lean_kernel<MFMA_MAIN, 2>,
               hamming_mfma_rows_kernel<MFMA_MAIN, 4>, (const int32_t*)(sampled ? tau_s : tau_p), none, none,
               p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
@@ -1519,7 +1777,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                        nq, rerun, qbflag, p.qpb);
     VRQ_LAUNCH_CHECK();
     if (p.rows)
-      rows_pass(hamming_mfma_rows_kernel<MFMA_RERUN, 1>, hamming_mfma_rows_kernel<MFMA_RERUN, 2>,
+      rows_pass(hamming_mfma_rows_kernel<MFMA_RERUN, 1>, hamming_mfma_rows_lean_kernel<MFMA_RERUN, 2>,
                 hamming_mfma_rows_kernel<MFMA_RERUN, 4>, (const int32_t*)tau_p, (const int32_t*)rerun,
                 (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
                 (int64_t)0);

@@ -42,6 +42,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 __device__ __forceinline__ void lds_read128(v4i& d, uint32_t a) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
+// the same read into a loop-carried register set: the destination is an in/out operand, so the read,
+// its wait and the loop-carried value form one tied chain the register allocator keeps in one place
+// (an output-only destination may be given other registers and copied into the carried ones before
+// the wait retires the load -- tests/isa_check.py)
+__device__ __forceinline__ void lds_read128_inplace(v4i& d, uint32_t a) {
+  asm volatile("ds_read_b128 %0, %1" : "+v"(d) : "v"(a) : "memory");
+}
 template <int OFF>
 __device__ __forceinline__ void lds_read128_imm(v4i& d, uint32_t a) {  // address + immediate offset
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
