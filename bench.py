@@ -431,12 +431,29 @@ def pmc_traffic(tag, kernel):
     """Per-launch HBM bytes of `kernel` from a committed rocprofv3 --pmc summary under profiles/
     (FETCH_SIZE KiB x2 for gfx950 16-B-per-lane streams + WRITE_SIZE KiB; tools/summarize_profile.py),
     or None when no summary for this workload tag is committed."""
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*{tag}*pmc*.json")))
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*{tag}*pmc*.json")), key=_round_key)
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
         return float(d["bytes_per_launch"][kernel])
+    except Exception:
+        return None
+
+
+def pmc_clock(tag, kernel, peak, achieved_at_events):
+    """The shader clock `kernel` ran at and its matrix-core busy fraction, from the committed clock pass
+    (GRBM_GUI_ACTIVE / 8 per launch over its rocprofv3 duration; SQ_VALU_MFMA_BUSY_CYCLES over 1024
+    SIMDs; MI355X_MICROARCH.md 'DVFS give-back'), and this run's rate as a fraction of the peak at
+    that clock.  None when no clock pass is committed for this workload."""
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*{tag}*pmc*.json")), key=_round_key)
+    try:
+        d = json.load(open(files[-1]))
+        c = d["clock"][kernel]
+        clk = float(c["eff_clock_ghz"])
+        return {"eff_clock_ghz": clk, "mfma_busy_frac": float(c["mfma_busy_frac"]),
+                "peak_at_clock": peak * clk / 2.4, "frac_at_clock": achieved_at_events / (peak * clk / 2.4),
+                "source": os.path.relpath(files[-1], HERE)}
     except Exception:
         return None
 
@@ -667,9 +684,11 @@ def run_c5(a, world, rank, dev):
     roof["frac"] = roof["achieved"] / roof["peak"]
     roof["rocprof"] = rocprof_field(tag, "gemm_topk_kernel<3, false, false>", ops, 1e12, I8_DENSE_PEAK_TOPS,
                                     st["cosine_main"])
+    roof["clock"] = pmc_clock(tag, "gemm_topk_kernel", I8_DENSE_PEAK_TOPS, roof["achieved"])
     roof_bin = {"achieved": ops / (st["binary_main"] * 1e-3) / 1e12, "kernel_ms": st["binary_main"],
                 "kernel": "gemm_topk_kernel<BINARY> main pass", "algorithmic_bytes_per_launch": m * 128}
     roof_bin["frac"] = roof_bin["achieved"] / roof["peak"]
+    roof_bin["clock"] = pmc_clock(tag, "gemm_topk_kernel_binary", I8_DENSE_PEAK_TOPS, roof_bin["achieved"])
     out = {
         "metric": METRIC, "value": nq * a.steps / T, "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": T / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
@@ -861,6 +880,7 @@ def phase1_leg(dev, n, nqs, k, osb, steps, warmup, threads, cpu=True, scan="auto
         tag = f"c3_n{n}_nq{nq}_g1"
         pt["rocprof"] = rocprof_field(tag, kern, mb, 1e9, HBM_PEAK_GBS, kms)
         pt["traffic"] = pmc_traffic(tag, "hamming_mfma_rows_kernel")
+        pt["clock"] = pmc_clock(tag, "hamming_mfma_rows_kernel", MFMA_FP4_PEAK_TOPS, pt["mfma"]["achieved"])
         points[str(nq)] = pt
         outs[nq] = (P.dist.cpu().numpy(), P.rows.cpu().numpy())
         del P
@@ -1106,6 +1126,7 @@ def run_3phase(a, world, rank, dev):
                 "measured_sustained_peak": measured_mfma_peak(), "rows": rows_m,
                 "prefix_rows_exact_scan": P.prefix_rows}
         roof["rocprof"] = rocprof_field(tag, kern, ops, 1e12, MFMA_FP4_PEAK_TOPS, st["matrix"])
+        roof["clock"] = pmc_clock(tag, _kname(kern), MFMA_FP4_PEAK_TOPS, ach)
         if nq <= 128:  # small batches (config-2 latency leg): K1r streams the codes, priced against HBM too
             mb = rows_m * 128 + nq * 128
             roof["hbm"] = {"achieved": mb / (st["matrix"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
