@@ -4,6 +4,7 @@ import ctypes as C
 import os
 import re
 
+import numpy as np
 import pytest
 
 from vectorragquantization_amd import _native as N
@@ -174,3 +175,23 @@ def test_no_copies_of_inflight_lds_reads(tmp_path):
     for o in objs:
         bad += isa_check.copies_of_inflight_lds_reads(isa_check.disassemble(o, str(tmp_path)))
     assert not bad, [f"{k}: {i} <- {ld}" for k, i, ld in bad[:4]]
+
+
+@pytest.mark.parametrize("nq,rows_kernel,mb", [(1, 1, 1), (32, 1, 1), (33, 1, 2), (64, 1, 2), (65, 1, 4),
+                                               (128, 1, 4), (129, 0, 2), (1024, 0, 4)])
+def test_scan_plan_picks_the_k1r_instance(nq, rows_kernel, mb):
+    """vrq_scan_plan (host-only) reports the matrix-core scan a batch runs: K1r with 1 / 2 / 4 M-blocks
+    per wave for <= 32 / 64 / 128 queries (the MB = 2 instance is the two-waves-per-SIMD lean kernel:
+    twice the chunks of the one-wave MB = 4 instance), K1m above; the chunks cover every row once and
+    the workspace holds the candidate lists, list lengths and thresholds it reports."""
+    lib = N.load()
+    n, K = 100_000_000, 100
+    info = np.zeros(12, np.int64)
+    N.check(lib.vrq_scan_plan(n, 1024, nq, K, 0, info.ctypes.data), "plan")
+    assert (int(info[0]), int(info[1])) == (rows_kernel, mb)
+    chunk_rows, nchunks, capc = int(info[2]), int(info[3]), int(info[4])
+    assert chunk_rows % 64 == 0 and (nchunks - 1) * chunk_rows < n <= nchunks * chunk_rows
+    if rows_kernel:  # one chunk per wave: 256 CUs x 4 waves x workgroups per CU
+        assert nchunks == 256 * 4 * (2 if mb <= 2 else 1)
+    off_cand, off_cnt, off_tau, ws = int(info[5]), int(info[6]), int(info[7]), int(info[11])
+    assert off_cand + nq * nchunks * capc * 8 <= off_cnt <= off_tau < ws
