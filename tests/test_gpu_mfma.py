@@ -190,12 +190,13 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib):
 def _sample_rows(n, nq):
     """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S = n/32 rows
     clamped to [32768, 2^20], as 64-row tiles spread at a tile stride ts >= 64 over the corpus, in
-    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass; 1024 chunks for <= 64 queries)."""
+    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass; for <= 64 queries the row-split
+    kernel's own sample pass: one chunk per wave, two workgroups of four waves per CU = 2048 chunks)."""
     nqb = (nq + 255) // 256
     S = min(max(n // 32, 32768), 1 << 20) if n // 32 <= (1 << 20) else 1 << 20
     tiles = min(max(S // 64, 1), n // 64)
-    # batches of <= 64 queries: the row-split kernel's sample pass, one chunk per wave (1024)
-    nsc = min(1024 if nq <= 64 else max(1, 256 // nqb), tiles)
+    # batches of <= 64 queries: the row-split kernel's sample pass, one chunk per wave (2048)
+    nsc = min(2048 if nq <= 64 else max(1, 256 // nqb), tiles)
     tiles = nsc * (tiles // nsc)
     ts = (n - 64) // (tiles - 1) if tiles > 1 else 64
     return (np.arange(tiles)[:, None] * ts + np.arange(64)[None, :]).reshape(-1)
