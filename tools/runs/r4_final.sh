@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 closing records: every GPU test, smoke, then rocprof/PMC/clock passes for c2 and c5.
+# Round-4 closing records: every GPU test, smoke, then (RUNS set) rocprof/PMC/clock passes.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r4final; mkdir -p $O
@@ -7,4 +7,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-RUNS="${RUNS:-c2:1024 c5:1024}" TAG=r4final_prof PMC=1 CLK=1 SQ=0 bash tools/prof.sh
+if [ -n "${RUNS:-}" ]; then RUNS="$RUNS" TAG=r4final_prof PMC=1 CLK=1 SQ=0 bash tools/prof.sh; fi
