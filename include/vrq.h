@@ -149,6 +149,13 @@ int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, 
  * order j, offset of the sorted K-lists, workspace bytes.  VRQ_EUNSUPPORTED when the shape takes the
  * wavefront scan. */
 int vrq_scan_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* info);
+/* Host-only introspection of the matrix-core scan's dense sample pass (tests and tools): info i64[6]
+ * = the row-split kernel runs it (1) or K1m's MB = 2 instance (0), sample chunks, rows per sample
+ * chunk, rows between consecutive sample chunks, rows between consecutive 64-row sample tiles, and
+ * the u16 lane-minimum columns per query at workspace offset 0 (32 per sample chunk: column
+ * chunk * 32 + r = min over the chunk's tiles and both 32-row halves of tile row r of
+ * dist - popcount(query), + 1024).  VRQ_EUNSUPPORTED when the shape takes the wavefront scan. */
+int vrq_scan_sample_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* info);
 
 /* ---------------------------------------------------------------------------
  * Merge of per-shard candidate tuples after the RCCL all-gather (multi-GPU
@@ -253,6 +260,15 @@ int vrq_gemm_topk_pieces(void);
  * per-(query, chunk) list capacity, query blocks, sample chunks, rows per sample chunk, workspace
  * bytes, queries per block.  VRQ_EUNSUPPORTED for shapes the path does not serve. */
 int vrq_gemm_topk_plan(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k, int64_t* info);
+/* Host-only introspection of the workspace layout (tests checking the candidate lists a MAIN stage
+ * leaves): info i64[8] = padded queries nq_pad; byte offsets of the per-query thresholds (f32
+ * [nq_pad], u units), the list lengths (i32 [nq][chunks]), the lists (u32 rows [nq][chunks][capc]) and
+ * the sample maxima (f32 [nq][cols]); sample columns per query, rows between sample chunks, rows per
+ * sample chunk.  The int8 query pieces a (q/S = a + rho) sit at offset 0 as i8 [nq_pad][1024]: natural
+ * dim order for VRQ_GEMM_INT8_COSINE, and within each 32-dim step the Phase-II k-permutation for
+ * VRQ_GEMM_BINARY.  Hit rule of the MAIN pass: binary u = <a, bits> >= ceil(thr); cosine u =
+ * f32(<a, x>) * (1 / f32(norm)) >= thr. */
+int vrq_gemm_topk_layout(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k, int64_t* info);
 int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
                   int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
                   int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,

@@ -161,7 +161,8 @@ def test_no_copies_of_inflight_lds_reads(tmp_path):
     """No kernel copies (or overwrites) a register that an inline-asm LDS read has not yet filled:
     the register allocator may move such a value with a v_mov placed before the s_waitcnt that
     retires the read (round 4: K1r's next-n-block rows, ~1 in 10^4 candidates with a wrong distance
-    on the GPU).  Checked on the disassembly of every built object (tests/isa_check.py)."""
+    on the GPU).  Checked on the disassembly of every built object along every static control-flow path
+(tests/isa_check.py; its own unit tests: tests/test_isa_check.py)."""
     import glob
     import shutil
     import isa_check
@@ -171,9 +172,13 @@ def test_no_copies_of_inflight_lds_reads(tmp_path):
         pytest.skip("no built objects or no ROCm llvm tools")
     if not shutil.which("objcopy") and not os.path.exists(os.path.join(isa_check.LLVM_BIN, "llvm-objcopy")):
         pytest.skip("no objcopy")
-    bad = []
+    bad, kernels, loads = [], 0, 0
     for o in objs:
-        bad += isa_check.copies_of_inflight_lds_reads(isa_check.disassemble(o, str(tmp_path)))
+        v, st = isa_check.scan(isa_check.disassemble(o, str(tmp_path)))
+        bad += v
+        kernels += st["kernels"]
+        loads += st["ds_loads"]
+    assert kernels >= 50 and loads >= 1000, (kernels, loads)  # the disassembly was parsed, not skipped
     assert not bad, [f"{k}: {i} <- {ld}" for k, i, ld in bad[:4]]
 
 

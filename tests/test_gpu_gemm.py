@@ -150,19 +150,32 @@ def test_gemm_topk_stage_split(dev):
         assert torch.equal(a, b)
 
 
-def test_gemm_topk_many_candidates(dev, monkeypatch):
-    """A small sample (VRQ_GEMM_SAMPLE_DIV, read only by the probe build libvrq_probe.so) and k = 100
-    leave thousands of candidates per query: the finish kernel's running top-k walks them in several
-    batches; the fallback stays off."""
+def test_gemm_topk_many_candidates(dev):
+    """k = 1000 leaves more than one finish batch (1024 rows) of candidates per query: the finish
+    kernel's running top-k walks them in several batches (checked on the lists the MAIN stage leaves);
+    the fallback stays off."""
     from vectorragquantization_amd import _native as N
-    monkeypatch.setenv("VRQ_GEMM_SAMPLE_DIV", "8")
-    probe = N.load_probe()
+    from vectorragquantization_amd.enhanced import gemm_topk
+    from vectorragquantization_amd.quant import int8_row_norms
+    lib = N.load()
     rng = np.random.default_rng(17)
-    n, nq, k = 200_000, 40, 100
+    n, nq, k = 200_000, 40, 1000
     F = _corpus(rng, n, 32)
     codes, x8, _ = O.encode_batch("cohere", F, 0.1)
     qf = _queries(rng, F, nq)
+    c_t, x_t, q_t = _t(codes, dev), _t(x8, dev), _t(qf, dev)
+    nrm = int8_row_norms(x_t)
     for mode in ("binary", "int8_cosine"):
-        cnt, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, flags=NOFB, lib=probe)
-        _check(mode, qf, k, cnt, rows, sc, codes=codes, x8=x8)
-
+        m = {"binary": N.VRQ_GEMM_BINARY, "int8_cosine": N.VRQ_GEMM_INT8_COSINE}[mode]
+        plan, lay = np.zeros(8, np.int64), np.zeros(8, np.int64)
+        N.check(lib.vrq_gemm_topk_plan(m, n, 1024, nq, k, plan.ctypes.data), "plan")
+        N.check(lib.vrq_gemm_topk_layout(m, n, 1024, nq, k, lay.ctypes.data), "layout")
+        nch, capc, off_cnt = int(plan[1]), int(plan[2]), int(lay[2])
+        ws = torch.zeros((int(plan[6]),), dtype=torch.uint8, device=dev)
+        for st in (N.VRQ_GEMM_STAGE_SAMPLE, N.VRQ_GEMM_STAGE_MAIN):
+            gemm_topk(mode, q_t, k, codes=c_t, x8=x_t, norms=nrm, flags=st, workspace=ws)
+        torch.cuda.synchronize()
+        cnt = ws[off_cnt:off_cnt + 4 * nq * nch].view(torch.int32).view(nq, nch)
+        assert int(cnt.clamp(max=capc).sum(1).min()) > 1024, mode
+        cnt_, rows, sc = _run(mode, qf, k, dev, codes=codes, x8=x8, flags=NOFB)
+        _check(mode, qf, k, cnt_, rows, sc, codes=codes, x8=x8)

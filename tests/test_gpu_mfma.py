@@ -87,11 +87,12 @@ def test_mfma_auto_selection_in_hamming_topk(dev, oracle_lib):
     assert np.array_equal(D0, D1) and np.array_equal(I0 * 3 + 1, L1)
 
 
-def test_mfma_heavy_ties(dev, oracle_lib):
+@pytest.mark.parametrize("nq", [8, 40, 64])          # K1r MB = 1 and the lean MB = 2 kernel
+def test_mfma_heavy_ties(dev, oracle_lib, nq):
     rng = np.random.default_rng(11)
     base = rng.integers(0, 256, (25, 128), dtype=np.uint8)
     codes = base[rng.integers(0, 25, 120_000)]            # every distance occurs thousands of times
-    qb = np.concatenate([base[:4], rng.integers(0, 256, (4, 128), dtype=np.uint8)])
+    qb = np.concatenate([base[:4], rng.integers(0, 256, (nq - 4, 128), dtype=np.uint8)])
     for K in (1, 100, 128):
         D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
         _, D1, I1 = _phase1(codes, qb, K, dev, "mfma", row_offset=5_000_000)
@@ -169,18 +170,21 @@ def test_mfma_and_valu_three_phase_identical(dev):
         assert np.array_equal(a, b, equal_nan=True) and np.array_equal(a, c, equal_nan=True)
 
 
-def test_mfma_hit_staging_overflow(dev, oracle_lib):
-    """64 queries (one wave's worth) and the whole suffix clustered around one code: every tile
-    gives a wave ~4096 hits, more than its LDS staging holds, so the lists are marked overflowed
-    and those queries are rescanned exactly; the other queries keep the fast path."""
+@pytest.mark.parametrize("nq", [200, 64, 40])      # K1m MB = 2; the lean MB = 2 K1r (full and partial)
+def test_mfma_hit_staging_overflow(dev, oracle_lib, nq):
+    """Up to 64 queries (one wave's worth) and the whole suffix clustered around one code: every tile
+    gives a wave thousands of hits, more than its LDS staging holds, so the lists are marked overflowed
+    and those queries are rescanned exactly; the other queries keep the fast path.  At 40 and 64 queries
+    this runs the lean K1r kernel's per-n-block stage overflow, spare-slot clamp and capc + 1 marking."""
     rng = np.random.default_rng(17)
-    n, nq, K = 100_000, 200, 100
+    n, K = 100_000, 100
     S = 32_768
     base = rng.integers(0, 256, (1, 128), dtype=np.uint8)
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     codes[S:] = _near(rng, np.repeat(base, n - S, axis=0), 6)
     qb = rng.integers(0, 256, (nq, 128), dtype=np.uint8)
-    qb[:64] = _near(rng, np.repeat(base, 64, axis=0), 4)
+    nh = min(nq, 64)
+    qb[:nh] = _near(rng, np.repeat(base, nh, axis=0), 4)
     D0, I0 = oracle_knn(oracle_lib, codes, qb, K)
     _, D1, I1 = _phase1(codes, qb, K, dev, "mfma")
     assert np.array_equal(D0, D1)

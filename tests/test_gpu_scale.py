@@ -1,10 +1,11 @@
 """BASELINE config 4 at full size on one GPU, the RCCL leg, and opening the reference's own DB folders.
 
-* 100M x 1024 corpus (SURVEY.md 8(d) generator): the three-phase search of one index equals, bit for
+* 100M x 1024 corpus (SURVEY.md 8(d) generator) at the bench's batch of nq = 1024 (the MB = 4
+  matrix-core kernel the headline number runs): the three-phase search of one index equals, bit for
   bit, the VRQ_SEARCH_SHARD searches of the 8 row ranges an 8-GPU run would own, merged by
   vrq_merge_shards (the multi-GPU semantics of CohereEnhancedVectorDB.py:267-322); the single index's
-  Phase I equals the FAISS hammings_knn_hc restatement and its final rows equal the reference NumPy
-  Phases II/III on a query sample.
+  Phase I equals the FAISS hammings_knn_hc restatement and its final rows and Phase-II scores equal the
+  reference NumPy Phases II/III on 16 queries spread over both 512-query blocks.
 * ShardedSearch through a real ``nccl`` (RCCL) process group.
 * ``CohereEnhancedVectorDB`` / ``CohereVectorDBFloat`` opening byte copies of the reference's persisted
   folders (tests/golden/ref_db: FAISS index + RocksDB tables) and reproducing its search output.
@@ -50,7 +51,7 @@ def test_100m_row_ranges_merge_equal_single_index(dev, oracle_lib):
     from vectorragquantization_amd.dist import merge_shards
     from vectorragquantization_amd.enhanced import search3
 
-    nq, k = 256, 10                          # nq >= 128: the matrix-core Phase-I path, as the bench runs
+    nq, k = 1024, 10                         # the bench's batch: K1m with 4 M-blocks per wave (2 query blocks)
     sh = synth.make_corpus(N100M, device=dev)
     codes, x8, norms = sh["codes"], sh["x8"], sh["norms"]
     qf, qb, _ = synth.make_queries(N100M, nq, device=dev)
@@ -65,15 +66,19 @@ def test_100m_row_ranges_merge_equal_single_index(dev, oracle_lib):
     for a, b in zip(merged, full):
         assert np.array_equal(a, b), "8 merged row ranges differ from the single 100M index"
     assert (full[0] == k).all()
+    info = np.zeros(12, np.int64)
+    N.check(N.load().vrq_scan_plan(N100M, 1024, nq, 100, 0, info.ctypes.data), "plan")
+    assert (int(info[0]), int(info[1])) == (0, 4)          # K1m, MB = 4: the instance the bench times
     # Phase I of the single index vs the FAISS restatement, and the final rows vs the reference NumPy
-    # Phases II/III on those candidates, for a query sample
-    qs = 8
+    # Phases II/III on those candidates, for 16 queries spread over both 512-query blocks
+    qsel = np.linspace(0, nq - 1, 16).round().astype(np.int64)
+    assert (qsel < 512).any() and (qsel >= 512).any()
     codes_h = codes.cpu().numpy()
-    D, I = oracle_knn(oracle_lib, codes_h, qb[:qs].cpu().numpy(), 100, threads=16)
-    assert np.array_equal(p1[2][:qs], D) and np.array_equal(p1[1][:qs], I)
+    D, I = oracle_knn(oracle_lib, codes_h, qb[torch.from_numpy(qsel).to(dev)].cpu().numpy(), 100, threads=16)
+    assert np.array_equal(p1[2][qsel], D) and np.array_equal(p1[1][qsel], I)
     qf_h = qf.cpu().numpy()
-    for q in range(qs):
-        rows = I[q]
+    for i, q in enumerate(qsel):
+        rows = I[i]
         x8r = x8[torch.from_numpy(rows).to(dev)].cpu().numpy()
         ref_rows, ref_s2 = _phase23_reference(qf_h[q], codes_h[rows], x8r, rows)
         assert np.array_equal(full[1][q], ref_rows)

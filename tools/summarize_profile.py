@@ -75,18 +75,30 @@ def main(src, dst, tag):
             continue
         out["bytes_per_launch"][k] = fetch + write
     # effective shader clock under load (GRBM_GUI_ACTIVE is the sum over the 8 XCDs) and the
-    # matrix-core busy fraction (SQ_VALU_MFMA_BUSY_CYCLES sums MFMA cycles over all 1024 SIMDs)
-    avg_ns = {}
-    for r in out.get("kernel_stats", []):
-        avg_ns.setdefault(short(r.get("Name", r.get("KernelName", ""))), float(r.get("AverageNs", 0) or 0))
+    # matrix-core busy fraction (SQ_VALU_MFMA_BUSY_CYCLES sums MFMA cycles over all 1024 SIMDs).  The
+    # duration is the per-dispatch mean after the warm-up steps (dispatch.json of the same run:
+    # tools/trace_dispatches.py) -- not the --stats average, which includes cold launches -- and a clock
+    # is reported only for kernels of >= 50 us and at most the 2.4 GHz maximum sclk (+5 %): shorter
+    # launches and their counter start/stop overheads give meaningless ratios.
+    dur_ns = {}
+    disp = os.path.join(src, "dispatch.json")
+    if os.path.exists(disp):
+        for name, v in json.load(open(disp)).get("kernels", {}).items():
+            dur_ns.setdefault(short(name), float(v["mean_after_warmup_ms"]) * 1e6)
     out["clock"] = {}
     for k, c in out.get("pmc_clk", {}).items():
         cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
         if cyc <= 0:
             continue
         d = {"cycles_per_xcd": cyc, "mfma_busy_frac": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * cyc)}
-        if avg_ns.get(k):
-            d["eff_clock_ghz"] = cyc / avg_ns[k]
+        ns = dur_ns.get(k)
+        if ns and ns >= 50e3:
+            clk = cyc / ns
+            if clk <= 2.4 * 1.05:
+                d["eff_clock_ghz"] = clk
+                d["duration_ns"] = ns
+            else:
+                d["eff_clock_invalid"] = clk
         out["clock"][k] = d
     if "hamming_scan_kernel" in out["bytes_per_launch"]:
         out["scan_bytes_per_launch"] = out["bytes_per_launch"]["hamming_scan_kernel"]

@@ -65,20 +65,32 @@ class _BuildLock:
         self.f.close()
 
 
-def _build_one(lib: str, probe: bool, verbose: bool) -> None:
+def _build_one(lib: str, probe: bool, verbose: bool, force_all: bool = False) -> None:
     hipcc = _hipcc()
     odir = os.path.join(OBJDIR, "probe") if probe else OBJDIR
     os.makedirs(odir, exist_ok=True)
+
+    headers = [d for d in _deps() if d.endswith(".h")]
 
     def compile_one(src):
         obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc, *CFLAGS, *(["-DVRQ_TUNING_ENV"] if probe else []), *EXTRA.get(src, []), "-c",
                os.path.join(CSRC, src), "-o", obj]
+        # incremental: an object newer than its source and every header, built by the same command
+        stamp = obj + ".cmd"
+        if not force_all and os.path.exists(obj) and os.path.exists(stamp):
+            t = os.path.getmtime(obj)
+            with open(stamp) as f:
+                same = f.read() == " ".join(cmd)
+            if same and all(os.path.getmtime(d) <= t for d in [os.path.join(CSRC, src), *headers]):
+                return obj
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
         if verbose and r.stderr:
             print(r.stderr, file=sys.stderr)
+        with open(stamp, "w") as f:
+            f.write(" ".join(cmd))
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
@@ -99,7 +111,7 @@ def build(force: bool = False, verbose: bool = False, probe: bool = False) -> st
         return lib
     with _BuildLock():
         if force or not up_to_date(lib):  # (another process may have built it while we waited)
-            _build_one(lib, probe, verbose)
+            _build_one(lib, probe, verbose, force_all=force)
     return lib
 
 

@@ -62,6 +62,7 @@ SIGNATURES = {
                                      _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "vrq_scan_kind": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
     "vrq_scan_plan": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
+    "vrq_scan_sample_plan": (C.c_int, [_I64, _I32, _I32, _I32, _I32, _P]),
     "vrq_merge_shards": (C.c_int, [_I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "vrq_rescore_binary": (C.c_int, [_P, _I32, _I32, _P, _I64, _P, _I32, _P, _P]),
     "vrq_rescore_int8_cosine": (C.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _I32, _P, _P]),
@@ -72,6 +73,7 @@ SIGNATURES = {
     "vrq_gemm_topk_workspace_size": (_SZ, [_I32, _I64, _I32, _I32, _I32]),
     "vrq_gemm_topk_pieces": (C.c_int, []),
     "vrq_gemm_topk_plan": (C.c_int, [_I32, _I64, _I32, _I32, _I32, _P]),
+    "vrq_gemm_topk_layout": (C.c_int, [_I32, _I64, _I32, _I32, _I32, _P]),
     "vrq_gemm_topk": (C.c_int, [_I32, _P, _P, _P, _I64, _I32, _I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _SZ,
                                 _P]),
     "vrq_flat_ip_prepare": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),

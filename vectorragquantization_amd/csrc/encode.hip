@@ -302,10 +302,6 @@ __global__ __launch_bounds__(EPB * 64) void encode_kernel(const void* __restrict
 //  * the code bytes from the LDS slice: lane l packs elements 16l..16l+15 (four conflict-free
 //    ds_read_b128) into bytes 2l, 2l+1 (one 128 B store per wave).
 constexpr int ENC_WPB = 4;                       // waves per workgroup (each on its own LDS slice)
-#ifndef VRQ_ENC_WGS_PER_CU
-#define VRQ_ENC_WGS_PER_CU 0                     // persistent workgroups per CU (0: one vector per wave)
-#endif
-constexpr bool kEncPersist = VRQ_ENC_WGS_PER_CU > 0;
 constexpr int ENC_SLICE = 1024 + 64;             // floats per wave slice (+ padding)
 
 // One butterfly step without the LDS crossbar (a __shfl_xor is a ds_bpermute round trip, ~100+
@@ -350,17 +346,9 @@ __device__ __forceinline__ float wave_allreduce(float x, OP op) {
 // Input rows by non-temporal loads (each f32 row is read once) for the modes where that measured
 // faster: int8g 0.66 -> 0.71, int16g 0.70 -> 0.71, Cohere 0.71 -> 0.72 of HBM; int4g and the local
 // modes measured 0.01-0.02 slower with it (tools/enc_probe.py, profiles/r3_encode_nt_variants.jsonl).
-// VRQ_ENC_NT (probe builds): 0 none, 1 every mode, 2 = this selection (the library default).
-#ifndef VRQ_ENC_NT
-#define VRQ_ENC_NT 2
-#endif
-#ifndef VRQ_ENC_LATE
-#define VRQ_ENC_LATE 0  // probe builds: 1 = the global modes quantise after the mean (no early stores)
-#endif
 template <int MODE>
 constexpr bool enc_nt() {
-  return VRQ_ENC_NT == 1 ||
-         (VRQ_ENC_NT == 2 && (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_INT16_GLOBAL || MODE == VRQ_ENC_COHERE));
+  return MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_INT16_GLOBAL || MODE == VRQ_ENC_COHERE;
 }
 template <int MODE>
 __device__ __forceinline__ void enc1024_load(float4 (&x)[4], const float* __restrict__ row, int l) {
@@ -383,11 +371,10 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
   __shared__ __attribute__((aligned(16))) float smem[ENC_WPB * ENC_SLICE];
   const int w = threadIdx.x >> 6, l = lane_id(), g = l >> 3, j = l & 7;
   float* xs = smem + w * ENC_SLICE;
-  const int64_t nw = (int64_t)gridDim.x * ENC_WPB;
-  int64_t v = (int64_t)blockIdx.x * ENC_WPB + w;
+  const int64_t v = (int64_t)blockIdx.x * ENC_WPB + w;  // one vector per wave
   if (v >= n) return;
-  float4 xn[4];
-  enc1024_load<MODE>(xn, xin + v * 1024, l);
+  float4 xc[4];
+  enc1024_load<MODE>(xc, xin + v * 1024, l);
   float lim = 0.f, gscale = 0.f;
   if constexpr (MODE == VRQ_ENC_INT8_GLOBAL || MODE == VRQ_ENC_COHERE) {
     lim = (float)limit;
@@ -396,11 +383,7 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
     lim = (float)limit;
     gscale = (float)(32767.0 / limit);
   }
-  for (; v < n; v += nw) {
-    float4 xc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) xc[k] = xn[k];
-    if (kEncPersist && v + nw < n) enc1024_load<MODE>(xn, xin + (v + nw) * 1024, l);  // next vector in flight
+  {
     float e[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -409,8 +392,6 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
       e[4 * k + 2] = xc[k].z;
       e[4 * k + 3] = xc[k].w;
     }
-    // previous vector's LDS reads are complete before the slice is overwritten
-    wave_lds_sync();
 #pragma unroll
     for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(xs + 256 * k + 4 * l) = xc[k];
     wave_lds_sync();
@@ -439,10 +420,6 @@ __global__ __launch_bounds__(ENC_WPB * 64) void encode1024_kernel(const float* _
         }
       }
       *reinterpret_cast<uint16_t*>(codes + v * 128 + 2 * l) = (uint16_t)bits;
-    }
-    if constexpr (VRQ_ENC_LATE) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e[i]) : "v"(mean));
     }
     float scale = gscale;
     bool flat = false;
@@ -592,15 +569,14 @@ int vrq_encode(int32_t mode, const void* x, int64_t n, int32_t dim, double limit
   if (dim == 1024 && mode != VRQ_ENC_BIN_INT16) {
     // one vector per wave (the measured best: 0.63-0.71 of HBM vs 0.58-0.61 for 4-6 persistent
     // workgroups per CU, tools/enc_probe.py), launches of at most 2^22 workgroups (2^24 vectors, a
-    // dispatch below 2^32 work-items); or VRQ_ENC_WGS_PER_CU persistent workgroups per CU, each
-    // wave looping over vectors
+    // dispatch below 2^32 work-items)
     const int64_t wgs = (n + ENC_WPB - 1) / ENC_WPB;
-    constexpr int64_t kPersist = 256 * VRQ_ENC_WGS_PER_CU, kMaxWgs = int64_t(1) << 22;
-    const int64_t lw = kEncPersist ? wgs : (wgs > kMaxWgs ? kMaxWgs : wgs);  // workgroups' vectors per launch
+    constexpr int64_t kMaxWgs = int64_t(1) << 22;
+    const int64_t lw = wgs > kMaxWgs ? kMaxWgs : wgs;  // workgroups' vectors per launch
     for (int64_t w0 = 0; w0 < wgs; w0 += lw) {
     const int64_t v0 = w0 * ENC_WPB, nv = n - v0 < lw * ENC_WPB ? n - v0 : lw * ENC_WPB;
     const int64_t g = (nv + ENC_WPB - 1) / ENC_WPB;
-    const dim3 grid((unsigned)(kEncPersist && g > kPersist ? kPersist : g)), block(ENC_WPB * 64);
+    const dim3 grid((unsigned)g), block(ENC_WPB * 64);
     const float* xf = (const float*)x + v0 * 1024;
     uint8_t* cv = codes + v0 * 128;
     void* qv = (uint8_t*)q + v0 * qrow;

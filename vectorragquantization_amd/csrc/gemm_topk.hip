@@ -1318,6 +1318,23 @@ extern "C" int vrq_gemm_topk_plan(int32_t mode, int64_t n, int32_t dim, int32_t 
   return VRQ_OK;
 }
 
+extern "C" int vrq_gemm_topk_layout(int32_t mode, int64_t n, int32_t dim, int32_t nq, int32_t k, int64_t* info) {
+  GemmPlan p;
+  if (!info) return VRQ_EINVAL;
+  if (!gemm_mode_ok(mode) || dim != DIM) return VRQ_EUNSUPPORTED;
+  const int rc = gemm_plan(n, nq, k, &p);
+  if (rc != VRQ_OK) return rc;
+  info[0] = p.nq_pad;
+  info[1] = (int64_t)p.off_thr;
+  info[2] = (int64_t)p.off_cnt;
+  info[3] = (int64_t)p.off_cand;
+  info[4] = (int64_t)p.off_dv;
+  info[5] = p.scols;
+  info[6] = p.sstride;
+  info[7] = p.scr;
+  return VRQ_OK;
+}
+
 extern "C" int vrq_gemm_topk(int32_t mode, const uint8_t* codes, const int8_t* x8, const double* norms, int64_t n,
                              int32_t dim, int64_t row_offset, const float* qf, int32_t nq, int32_t k, int32_t flags,
                              int32_t* out_count, int64_t* out_rows, double* out_scores, void* workspace,

@@ -488,6 +488,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     constexpr int g = decltype(G)::value;
     lds_read128_imm<g * 1024>(ring[g], bl0);
   });
+  // ntiles >= 1 (row0 < row1 above): no zero-trip path on which the seed and B-fragment reads issued
+  // above would stay in flight into the epilogue (tests/isa_check.py follows every static path)
+  __builtin_assume(ntiles > 0);
   for (int t = 0; t < ntiles; ++t) {
     store_flushed();                       // previous tile's first 64 hits
     if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 // ~1 in 10^4 candidates; tests/test_capi.py::test_no_copies_of_inflight_lds_reads checks the ISA.)
 template <int MB>
 struct RowsShape {
-  static_assert(MB == 1 || MB == 2 || MB == 4, "M-blocks per wave");
+  static_assert(MB == 1 || MB == 4, "M-blocks per wave (MB = 2: hamming_mfma_rows_lean_kernel)");
   static constexpr int QPW = 32 * MB;
   static constexpr int OCC = MB == 1 ? 2 : 1;  // workgroups (of MWAVES single-wave chunks) per CU
   static constexpr int NPR = MB == 1 ? 2 : 3;  // packed ring depth per wave (tile t+NPR-1 in flight)
@@ -1054,13 +1057,14 @@ template <int MB>
 struct LeanShape {
   static_assert(MB == 2, "lean K1r: the MB = 2 instance");
   static constexpr int QPW = 32 * MB;
+  static constexpr int OCC = 2;  // workgroups per CU (two waves per SIMD); mfma_plan sizes the chunks by it
   static constexpr int NPR = 2;
   static constexpr int SMEM = MWAVES * (NPR * PKT + QPW * 8 + (STG + 1) * 4 + MB * 128);
-  static_assert(2 * SMEM <= 160 * 1024, "LDS budget of two workgroups per CU");
+  static_assert(OCC * SMEM <= 160 * 1024, "LDS budget of two workgroups per CU");
 };
 
 template <int MODE, int MB>
-__global__ __launch_bounds__(MWAVES * 64, 2) void hamming_mfma_rows_lean_kernel(
+__global__ __launch_bounds__(MWAVES * 64, LeanShape<MB>::OCC) void hamming_mfma_rows_lean_kernel(
     const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
@@ -1637,7 +1641,7 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
     p->nqb = 1;
-    rows_occ = p->mb == 1 ? RowsShape<1>::OCC : p->mb == 2 ? 2 /* lean */ : RowsShape<4>::OCC;
+    rows_occ = p->mb == 1 ? RowsShape<1>::OCC : p->mb == 2 ? LeanShape<2>::OCC : RowsShape<4>::OCC;
   }
   // the dense sample pass always runs the MB = 2 instance (its 16 stores per block would spill at MB = 4)
   p->nqb_s = (nq + MfmaShape<kMbSmall>::QPB - 1) / MfmaShape<kMbSmall>::QPB;
@@ -1743,8 +1747,10 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                          qf, d, dstride);
   };
   if ((st & VRQ_SCAN_STAGE_PREFIX) && p.rows_sample) {  // dense sample pass (K1r) + per-query thresholds
+    // (rows_sample implies MB <= 2: the MB = 1 instance fills the unreachable MB = 4 slot)
+    if (p.mb > 2) return VRQ_EUNSUPPORTED;
     rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_lean_kernel<MFMA_SAMPLE, 2>,
-              hamming_mfma_rows_kernel<MFMA_SAMPLE, 2>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
+              hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
               p.sample_stride, p.sample_tile_stride, dv, p.dvcols);
     VRQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(sample_select_kernel, dim3(nq), dim3(256), 0, s, (const uint16_t*)dv, p.dvcols, q, K, p.j,

@@ -279,14 +279,17 @@ __global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* _
   v4u rA[C], rB[C];
   read_tile(0, rA);
   wait_tile(rA);
+  // (The LDS reads of the next tile are issued and retired on every path, the last iteration's
+  // included -- where they read a stale ring slot that nothing uses -- so that no read is ever in
+  // flight on a path that skips its wait: tests/isa_check.py follows every static path.)
   for (int t = 0; t < ntiles; t += 2) {
     // ---- tile t from A, prefetch t+1 into B
     if (t + 1 < ntiles) {
       if (t + 2 < ntiles) wait_vmcnt<GPW>(); else wait_vmcnt<0>();
       lds_barrier();
-      read_tile(t + 1, rB);
-      if (t + 3 < ntiles) issue(t + 3);
     }
+    read_tile(t + 1, rB);
+    if (t + 3 < ntiles) issue(t + 3);
     {
       const int local = t * 64 + l;
       uint32_t da, db;
@@ -294,15 +297,15 @@ __global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* _
       if (nqa > 0) accept(0, local < nrows ? ((da << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
       if (QG == 2 && nqa > 1) accept(1, local < nrows ? ((db << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
     }
-    if (t + 1 >= ntiles) break;
     wait_tile(rB);
+    if (t + 1 >= ntiles) break;
     // ---- tile t+1 from B, prefetch t+2 into A
     if (t + 2 < ntiles) {
       if (t + 3 < ntiles) wait_vmcnt<GPW>(); else wait_vmcnt<0>();
       lds_barrier();
-      read_tile(t + 2, rA);
-      if (t + 4 < ntiles) issue(t + 4);
     }
+    read_tile(t + 2, rA);
+    if (t + 4 < ntiles) issue(t + 4);
     {
       const int local = (t + 1) * 64 + l;
       uint32_t da, db;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(64 * WPG) void hamming_scan_kernel(const uint8_t* _
       if (nqa > 0) accept(0, local < nrows ? ((da << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
       if (QG == 2 && nqa > 1) accept(1, local < nrows ? ((db << LOCAL_BITS) | (uint32_t)local) : 0xffffffffu);
     }
-    if (t + 2 < ntiles) wait_tile(rA);
+    wait_tile(rA);
   }
 
   // chunk done: exact top-K per query -> global keys (dist << 40 | shard row), padded.

@@ -655,6 +655,22 @@ int vrq_scan_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, 
   return VRQ_OK;
 }
 
+int vrq_scan_sample_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* info) {
+  if (!info || n < 1 || nq < 1 || K < 1) return VRQ_EINVAL;
+  if (dim != DIM || K > KMAX) return VRQ_EUNSUPPORTED;
+  if (!mfma_use(n, nq, K, flags)) return VRQ_EUNSUPPORTED;
+  MfmaPlan p;
+  const int rc = mfma_plan(n, nq, K, &p);
+  if (rc != VRQ_OK) return rc;
+  info[0] = p.rows_sample;
+  info[1] = p.sample_chunks;
+  info[2] = p.sample_chunk_rows;
+  info[3] = p.sample_stride;
+  info[4] = p.sample_tile_stride;
+  info[5] = p.dvcols;
+  return VRQ_OK;
+}
+
 int vrq_merge_shards(int32_t nshards, int32_t nq, int32_t K, const int32_t* counts, const int64_t* rows,
                      const int32_t* dist, const double* s2, const double* s3, int32_t k, int32_t K3,
                      int32_t* out_count, int64_t* out_rows, int32_t* out_dist, double* out_binary,
