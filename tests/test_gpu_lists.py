@@ -126,8 +126,12 @@ def test_scan_candidate_lists_exact(dev, nq, inst):
     assert (d_true < tau[qs]).all()
     # every list complete: the listed (q, row) set is exactly {dist < tau}, each row once
     listed = torch.sort(qs * n + rows).values
-    tq, tr = torch.nonzero(D < tau[:, None].to(torch.int16), as_tuple=True)
-    assert torch.equal(listed, tq * n + tr), f"{listed.numel()} listed vs {tq.numel()} rows below the thresholds"
+    want = []
+    for q0 in range(0, nq, 128):  # (torch.nonzero of > 2^31 elements fails: query blocks)
+        tq, tr = torch.nonzero(D[q0:q0 + 128] < tau[q0:q0 + 128, None].to(torch.int16), as_tuple=True)
+        want.append((tq + q0) * n + tr)
+    want = torch.cat(want)
+    assert torch.equal(listed, want), f"{listed.numel()} listed vs {want.numel()} rows below the thresholds"
     assert (cnt.sum(1) >= K).all()  # the recheck's guarantee: tau_s admitted >= K rows, or the query re-ran with tau_p
 
 
