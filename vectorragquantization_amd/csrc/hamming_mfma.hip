@@ -137,6 +137,32 @@ constexpr int ENT_V_SHIFT = 14, ENT_Q_SHIFT = 7, ENT_V_BIAS = 1025;
 // (gi = 20+MB and 24+MB).
 enum { MFMA_MAIN = 0, MFMA_SAMPLE = 1, MFMA_RERUN = 2 };
 
+// The per-group LDS wait of the schedule above.  Group gi consumes the B fragment read at the top of
+// group gi - BAHEAD; DS operations complete in order, so the wait may leave in flight exactly the DS
+// operations issued after that read: the B reads of the groups since, and every other LDS operation
+// of those groups on the no-hit path (a hit adds stage writes, which only makes the counted wait
+// stricter).  Per group g: pre(g) = reads issued after its B read and before its wait (packed unit,
+// row popcounts), post(g) = operations issued in its slots (unpack writes, the popcount write, four
+// accumulator-seed reads, the two hit-flush steps).  Groups gi < BAHEAD read tiles the previous
+// iteration's lgkmcnt(0) retired: their wait counts this iteration's operations so far.  Capped at 15
+// (the counter's range; a smaller count only waits longer).
+#ifndef VRQ_K1M_EXACT_WAIT
+#define VRQ_K1M_EXACT_WAIT 1
+#endif
+constexpr int k1m_pre(int g) { return ((g & 7) == 1 ? 1 : 0) + (g == 12 ? 2 : 0); }
+constexpr int k1m_post(int g, int mb, bool dense) {
+  const int j = g & 15;
+  return ((g & 7) == 6 ? 2 : 0) + (g == 28 ? 1 : 0) + (!dense && j >= 4 + mb && j < 4 + 2 * mb ? 4 : 0) +
+         (!dense && g == 20 + mb ? 1 : 0) + (!dense && g == 24 + mb ? 1 : 0);
+}
+constexpr int k1m_wait(int gi, int mb, bool dense) {
+  if (!VRQ_K1M_EXACT_WAIT) return BAHEAD;
+  const int g0 = gi - BAHEAD;
+  int n = 1 + k1m_pre(gi);  // this group's B read and pre-wait reads
+  for (int g = g0 < 0 ? 0 : g0; g < gi; ++g) n += (g == g0 ? 0 : 1) + k1m_pre(g) + k1m_post(g, mb, dense);
+  return n < 15 ? n : 15;
+}
+
 // The dense sample pass keeps, per lane and accumulator register, the minimum of v = dist - pc(q)
 // over the sample rows of its chunk that the lane holds (lane row ri of every n-block): 32 values
 // per (query, chunk), each the distance of a DISTINCT sample row, written once per chunk as u16
@@ -517,11 +543,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
         lds_read128(pa, pks + psrc0);
         lds_read128(pb, pks + psrc1);
       }
-      // everything but the BAHEAD most recent LDS operations has completed: the fragment of
-      // this group (read BAHEAD groups ago), the packed unit read 5 groups ago, the popcounts
+      // every LDS operation issued up to the B read of group gi - BAHEAD has completed (k1m_wait): the
+      // fragment of this group, the packed unit read 5 groups ago, the popcounts, the seeds
       asm volatile("s_waitcnt lgkmcnt(%7)"
                    : "+v"(ring[gi & (NRING - 1)]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb), "+v"(fe)
-                   : "n"(BAHEAD)
+                   : "n"(k1m_wait(gi, MB, DENSE))
                    : "memory");
       // The group's non-MFMA work is cut into four slots that sit between its MFMAs (slot k after
       // MFMA k; at MB = 2 slots 2k and 2k+1 after MFMA k): an in-order wave issues them while the
@@ -599,7 +625,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             asm volatile("" ::"v"(pc0));
           } else {
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-            if ((l & 3) == 0) lds_write32(pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4 + pr * 4), pc0);
+            // every lane of the quad writes the same sum (no exec-masked branch: the counted waits
+            // above assume this write is issued on every path)
+            lds_write32(pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4 + pr * 4), pc0);
           }
         }
         if constexpr (SEED) {  // one 16-byte piece of M-block sm's seeds per slot, into its accumulator
