@@ -231,6 +231,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   if (chunk >= nchunks) return;
   // re-run pass (exact fallback of the sampled threshold): only query blocks with a failed query
   if (qbflag && qbflag[qb] == 0) return;
+#ifdef VRQ_K1M_STAMPS  // diagnostic build only (tools/probes/k1m_stamps.py): per-workgroup timeline
+  const uint64_t st_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const int64_t row0 = row_begin + (int64_t)chunk * chunk_stride;
   // strided (sample pass): tile t starts at row0 + t * tile_stride, every tile whole (the plan keeps
   // the last one inside the corpus); otherwise the chunk is rows [row0, row0 + chunk_rows)
@@ -510,6 +513,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       load_seed(acc[1][m], m);
     });
   barrier_all();  // B_0: unpacked tiles 0 and 1, packed tile 2 visible
+#ifdef VRQ_K1M_STAMPS
+  const uint64_t st_loop = __builtin_amdgcn_s_memrealtime();
+#endif
   static_for<0, BAHEAD>([&](auto G) {
     constexpr int g = decltype(G)::value;
     lds_read128_imm<g * 1024>(ring[g], bl0);
@@ -721,6 +727,15 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     if (nst) flush_from(0, row0 + (int64_t)(ntiles - 2) * RT);
   }
   wait_lgkm0();
+#ifdef VRQ_K1M_STAMPS
+  if (!DENSE && threadIdx.x == 0) {  // the MAIN pass gets the workspace head as `dv` in this build
+    uint64_t* stp = reinterpret_cast<uint64_t*>(dv) + 4 * (int64_t)L;
+    stp[0] = st_start;
+    stp[1] = st_loop;
+    stp[2] = __builtin_amdgcn_s_memrealtime();
+    stp[3] = ((uint64_t)__builtin_amdgcn_s_getreg(63508) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(63492);
+  }
+#endif
   if constexpr (DENSE)
     dmin.out(dv, dv_stride, (int64_t)chunk * 32 + ri, qbase, h, nq);
   else
@@ -1800,9 +1815,14 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
               p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   } else if (st & VRQ_SCAN_STAGE_MATRIX) {
+#ifdef VRQ_K1M_STAMPS
+    uint16_t* mdv = dv;
+#else
+    uint16_t* mdv = nullptr;
+#endif
     pass(hamming_mfma_kernel<MFMA_MAIN, kMbLarge>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
          (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
-         (uint16_t*)nullptr, (int64_t)0);
+         mdv, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_RECHECK) && sampled) {
