@@ -30,9 +30,9 @@
 //    K-list per query, exactly in every case (overflow -> exact rescan).
 #include <stdlib.h>
 
-#include "mfma_common.h"
-#include "vrq_internal.h"
-#include "vrq_scan.h"
+#include "../../../vectorragquantization_amd/csrc/mfma_common.h"
+#include "../../../vectorragquantization_amd/csrc/vrq_internal.h"
+#include "../../../vectorragquantization_amd/csrc/vrq_scan.h"
 
 namespace vrq {
 
@@ -1345,6 +1345,297 @@ __global__ __launch_bounds__(MWAVES * 64, LeanShape<MB>::OCC) void hamming_mfma_
       if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
 }
 
+// K1r for 33..64 queries on the 16x16x128 FP4 shape (round 5).  The chip holds a higher clock under
+// v_mfma_scale_f32_16x16x128_f8f6f4 than under 32x32x64 for the same work (tools/probes/
+// mfma_fp4_shape_rate.hip: 2.37 vs 2.05-2.12 GHz on this kernel's loop; profiles/r5_mfma_shape_rate_
+// probes.jsonl), and this scan runs well below 2.4 GHz (1.82 GHz at 100M rows, nq = 64).  Per wave 64
+// queries = 4 query blocks of 16, per 32-row n-block 2 row blocks of 16 and 8 k-steps of 128 dims;
+// the resources match the 32x32 lean kernel (A 128 AGPRs, 32 accumulator registers, 16 packed-row
+// registers, two waves per SIMD), the accumulator seeds need 16 registers instead of 32.
+//   lane l: rr = l & 15, g = l >> 4.  A[m][s]: query 16 m + rr, B[nb]: tile row 16 nb + rr; both take
+//   code word 4 P(g) + s (32 dims), P = 0, 6, 2, 4 for g = 0..3: lane group g reads 16-B pieces P, P + 1
+//   of its row (conflict-free in every ds_read_b128 lane group of the swizzled tile image).
+//   C: [query 16 m + 4 g + i][tile row 16 nb + rr], i = 0..3.
+__device__ __forceinline__ v4f mfma_fp4_16(const v4i& a, const v4i& b, const v4f& c) {
+  const v8i a8 = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
+  const v8i b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, FMT_FP4, FMT_FP4, 0, 0, 0, 0);
+}
+__device__ __forceinline__ int r16_piece(int g) { return (0x4260 >> (4 * g)) & 0xF; }
+// sum of a lane value over the four lane groups g (lanes rr, rr + 16, rr + 32, rr + 48)
+__device__ __forceinline__ int sum_over_groups(int x) {
+  const auto p = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)x, false, false);
+  const int y = (int)(p[0] + p[1]);
+  const auto q = __builtin_amdgcn_permlane16_swap((uint32_t)y, (uint32_t)y, false, false);
+  return (int)(q[0] + q[1]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(MWAVES * 64, LeanShape<2>::OCC) void hamming_mfma_rows16_kernel(
+    const uint8_t* __restrict__ codes, int64_t n, const uint8_t* __restrict__ queries, int nq,
+    const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
+    int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, const int32_t* __restrict__ rerun,
+    const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
+  constexpr bool DENSE = MODE == MFMA_SAMPLE;
+  constexpr int QB = 4, QPW = 64, NPR = LeanShape<2>::NPR, KS8 = 8;
+  if (qbflag && qbflag[0] == 0) return;  // re-run pass with no failed query
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LeanShape<2>::SMEM];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* pk = smem + w * (NPR * PKT);  // this wave's ring
+  int32_t* wbase = reinterpret_cast<int32_t*>(smem + MWAVES * NPR * PKT);
+  int32_t* lcnt = wbase + w * QPW;
+  int32_t* tq = wbase + MWAVES * QPW + w * QPW;
+  int32_t* stg = wbase + 2 * MWAVES * QPW + w * (STG + 1);
+  float* sd = reinterpret_cast<float*>(wbase + 2 * MWAVES * QPW + MWAVES * (STG + 1)) + w * QPW;
+  const int l = lane_id();
+  const int rr = l & 15, g = l >> 4;
+  const int nb_ = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3, q8 = nb_ >> 3, r8 = nb_ & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int chunk = L * MWAVES + w;
+  if (chunk >= nchunks) return;
+  const int64_t row0 = (int64_t)chunk * chunk_stride;
+  const bool strided = tile_stride != RT;
+  const int64_t row1 = strided ? n : (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
+  if (row0 >= row1) return;
+  const int nrows = strided ? (int)chunk_rows : (int)(row1 - row0);
+  const int ntiles = (nrows + RT - 1) / RT;
+  const int nblk = 2 * ntiles;
+
+  // LDS-DMA of packed tile t (as hamming_mfma_rows_lean_kernel)
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    int lo_ = l;
+    asm volatile("" : "+v"(lo_));
+    const uint32_t lo0 = (uint32_t)((lo_ >> 3) * 128 + ((lo_ & 7) ^ (lo_ >> 4)) * 16);
+    uint8_t* buf = pk + (t % NPR) * PKT;
+    const int64_t tr0 = row0 + (int64_t)t * tile_stride;
+    const bool whole = tr0 + RT <= row1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t off = lo0 ^ (uint32_t)((i & 1) * 64);
+      int64_t row = tr0 + 8 * i + (int64_t)(off >> 7);
+      if (!whole) row = row < row1 ? row : row1 - 1;
+      const uint8_t* src = codes + row * 128 + (off & 127);
+      uint8_t* dst = buf + i * 1024;
+      if (whole)
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, K1R_AUX);
+      else
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  for (int t = 0; t < NPR && t < ntiles; ++t) issue(t);
+
+  // A fragments: query 16 m + rr, word 4 P(g) + s of the query (32 dims as e2m1 0/1 values)
+  const int P = r16_piece(g);
+  v4i A[QB][KS8];
+#pragma unroll
+  for (int m = 0; m < QB; ++m) {
+    const int q = 16 * m + rr;
+    const bool qok = q < nq && (!rerun || rerun[q]);
+    const uint32_t* qp = reinterpret_cast<const uint32_t*>(queries + (int64_t)(qok ? q : 0) * 128);
+    int pc = 0;
+#pragma unroll
+    for (int s = 0; s < KS8; ++s) {
+      const uint32_t wd = qok ? qp[4 * P + s] : 0u;
+      pc += __popc(wd);
+      A[m][s] = unpack_query32(wd);
+    }
+    pc = sum_over_groups(pc);  // the four lane groups hold disjoint words of the query
+    if (g == 0) tq[q] = DENSE ? 0 : qok ? tau[q] - pc : -0x40000000;
+  }
+#pragma unroll
+  for (int m = 0; m < QB; ++m)
+#pragma unroll
+    for (int s = 0; s < KS8; ++s) asm volatile("" : "+a"(A[m][s]));
+  for (int i = l; i < QPW; i += 64) lcnt[i] = 0;
+  // seeds tau'/2 in query order: lane (rr, g) of query block m needs queries 16 m + 4 g .. + 3
+  sd[l] = 0.5f * (float)tq[l];
+  const uint32_t sd0 = lds_addr(sd) + (uint32_t)(g * 16), stg0 = lds_addr(stg);
+  const uint32_t lc0 = lds_addr(lcnt), pk0 = lds_addr(pk);
+  v4f seedv[QB];
+  if constexpr (!DENSE) {
+    v4i p[QB];
+#pragma unroll
+    for (int m = 0; m < QB; ++m) lds_read128(p[m], sd0 + (uint32_t)(m * 64));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3])::"memory");
+#pragma unroll
+    for (int m = 0; m < QB; ++m) seedv[m] = __builtin_bit_cast(v4f, p[m]);
+  }
+  // piece i of the lane's 32 bytes of row (32 (blk & 1) + 16 nb + rr) of n-block blk's packed tile
+  auto read_piece = [&](v4i& d, int nb, int i, int blk) __attribute__((always_inline)) {
+    const int r = 32 * (blk & 1) + 16 * nb + rr;
+    lds_read128_inplace(d, pk0 + (uint32_t)(((blk >> 1) % NPR) * PKT) + (uint32_t)(pk_slot(r, P + i) * 16));
+  };
+  auto wait_tiles = [&](int k) __attribute__((always_inline)) {
+    if (k <= 0) wait_vm<0>();
+    else wait_vm<8>();
+  };
+  wait_tiles((ntiles < NPR ? ntiles : NPR) - 1);  // tile 0 landed
+  v4i rb[2][2];  // [row block][piece]
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) read_piece(rb[nb][i], nb, i, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[0][0]), "+v"(rb[0][1]), "+v"(rb[1][0]), "+v"(rb[1][1])::"memory");
+
+  const int64_t qstride = (int64_t)nchunks * capc;
+  uint64_t* const cbase = cand + (int64_t)chunk * capc;
+  int nst = 0;
+  auto flush_all = [&](int64_t base_row) __attribute__((always_inline)) {
+    if (nst > STG) {
+      for (int i = l; i < QPW; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
+      nst = STG;
+    }
+    for (int i0 = 0; i0 < nst; i0 += 64) {
+      const int i = i0 + l;
+      int e = 0, pos = 0;
+      if (i < nst) lds_read32(e, stg0 + (uint32_t)(i * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e)::"memory");
+      const int ql = (e >> ENT_Q_SHIFT) & 127;
+      if (i < nst) lds_add_rtn32(pos, lc0 + (uint32_t)(ql * 4), 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pos)::"memory");
+      if (i < nst && pos < capc)
+        cbase[(int64_t)ql * qstride + pos] =
+            ((uint64_t)(uint32_t)(e >> ENT_V_SHIFT) << KEY_ROW_BITS) | (uint64_t)(base_row + (e & 127));
+    }
+    nst = 0;
+  };
+  // hits of row block nb (its threshold hp, row popcount pc) of the n-block: one ballot per (m, i)
+  auto block_hits = [&](const v4f (&acc)[QB][2], int nb, int pc, float hp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < QB; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t mask = __ballot(acc[m][nb][i] > hp);
+        if (mask) {
+          if ((mask >> l) & 1) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+            int lo = l;
+            asm volatile("" : "+v"(lo));
+            const int ql = 16 * m + 4 * (lo >> 4) + i;
+            const int v = pc - (int)(2.0f * acc[m][nb][i]);  // dist - tau(q)
+            const int pos = nst + below < STG ? nst + below : STG;
+            lds_write32(stg0 + (uint32_t)(pos * 4),
+                        ((v + ENT_V_BIAS) << ENT_V_SHIFT) | (ql << ENT_Q_SHIFT) | (16 * nb + (lo & 15)));
+          }
+          nst += __popcll(mask);
+        }
+      }
+  };
+  // DENSE: lane minima of v = dist - pc(q) per (query block, row block, register)
+  float dmin[DENSE ? QB : 1][2][4];  // (as DenseMin: float minima, +inf = no row)
+  if constexpr (DENSE) {
+#pragma unroll
+    for (int m = 0; m < QB; ++m)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dmin[m][nb][i] = __builtin_inff();
+  }
+  v4f acc[QB][2];
+  for (int blk = 0; blk < nblk; ++blk) {
+    // entering the second n-block of tile t: the next n-block's pieces come from tile t + 1
+    if ((blk & 1) && blk + 1 < nblk) {
+      const int t1 = (blk + 1) >> 1;
+      const int last = t1 + NPR - 1 < ntiles ? t1 + NPR - 1 : ntiles - 1;
+      wait_tiles(last - t1);
+    }
+    const int nx = blk + 1 < nblk ? blk + 1 : blk;
+    int pcs[2] = {0, 0};
+    static_for<0, KS8>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      static_for<0, 2>([&](auto NB) {
+        constexpr int nb = decltype(NB)::value;
+        const uint32_t wd = (uint32_t)rb[nb][s >> 2][s & 3];
+        const v4i bfrag = unpack_row32(wd);
+        static_for<0, QB>([&](auto M) {
+          constexpr int m = decltype(M)::value;
+          if constexpr (s == 0 && DENSE)
+            acc[m][nb] = mfma_fp4_16(A[m][s], bfrag, v4f{});
+          else if constexpr (s == 0)
+            acc[m][nb] = mfma_fp4_16(A[m][s], bfrag, seedv[m]);
+          else
+            acc[m][nb] = mfma_fp4_16(A[m][s], bfrag, acc[m][nb]);
+          asm volatile("" : "+v"(acc[m][nb]));
+        });
+        VRQ_SCHED_FENCE();
+        pcs[nb] += __popc(wd);
+      });
+      // piece (s >> 2) of both row blocks consumed: read the next n-block's (unconditional: the last
+      // n-block re-reads its own rows, unused -- a read under a branch would merge register sets at the
+      // join by copies the allocator may place before the wait)
+      if constexpr ((s & 3) == 3) {
+        read_piece(rb[0][s >> 2], 0, s >> 2, nx);
+        read_piece(rb[1][s >> 2], 1, s >> 2, nx);
+      }
+      VRQ_SCHED_FENCE();
+    });
+    // epilogue of this n-block: row popcounts (the four lane groups hold disjoint words of a row)
+    const int lr0 = blk * 32 + rr;
+    int prow[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) prow[nb] = sum_over_groups(pcs[nb]);
+    if constexpr (DENSE) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const float pcf = lr0 + 16 * nb < nrows ? (float)prow[nb] : __builtin_inff();
+#pragma unroll
+        for (int m = 0; m < QB; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dmin[m][nb][i] = fminf(dmin[m][nb][i], fmaf(-2.0f, acc[m][nb][i], pcf));
+      }
+    } else {
+      int pc[2];
+      float hp[2];
+      uint64_t any = 0;
+      uint64_t hitm[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        pc[nb] = lr0 + 16 * nb < nrows ? prow[nb] : 0x40000000;
+        hp[nb] = 0.5f * (float)pc[nb];
+        const int hpb = __float_as_int(hp[nb]);
+        int x[QB];
+#pragma unroll
+        for (int m = 0; m < QB; ++m) {
+          const v4i bb = __builtin_bit_cast(v4i, acc[m][nb]);
+          x[m] = max(max(bb.x, bb.y), max(bb.z, bb.w));
+        }
+        hitm[nb] = __ballot(max(max(x[0], x[1]), max(x[2], x[3])) > hpb);
+        any |= hitm[nb];
+      }
+      if (any) {  // rare
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          if (hitm[nb]) block_hits(acc, nb, pc[nb], hp[nb]);
+        if (nst) flush_all(row0 + (int64_t)blk * 32);
+      }
+    }
+    // the next n-block's rows landed (every destination named)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[0][0]), "+v"(rb[0][1]), "+v"(rb[1][0]), "+v"(rb[1][1])::"memory");
+    // after n-block 2t every read from tile t is retired: its ring slot takes the DMA of tile t + NPR
+    if (!(blk & 1) && (blk >> 1) + NPR < ntiles) issue((blk >> 1) + NPR);
+  }
+  wait_lgkm0();
+  if constexpr (DENSE) {
+#pragma unroll
+    for (int m = 0; m < QB; ++m)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 16 * m + 4 * g + i;
+          const float v = dmin[m][nb][i];
+          if (q < nq)
+            dv[(int64_t)q * dv_stride + (int64_t)chunk * 32 + 16 * nb + rr] =
+                v == __builtin_inff() ? (uint16_t)0xFFFF : (uint16_t)((int)v + 1024);
+        }
+  } else {
+    for (int i = l; i < QPW; i += 64)
+      if (i < nq && (!rerun || rerun[i])) ccnt[(int64_t)i * nchunks + chunk] = lcnt[i];
+  }
+}
+
 // Thresholds from the dense sample (S rows spread over the corpus, every distance exact):
 //   tau_p(q) = d_(K) + 1, accept dist <= the K-th smallest sample distance: the sample rows alone
 //              put >= K corpus rows under it, so the candidates always hold the exact top-K
@@ -1753,6 +2044,14 @@ bool mfma_use(int64_t n, int nq, int K, int flags) {
   return ok && nq >= kMfmaMinQueries;  // K1r serves even one query faster than the wavefront scan
 }
 
+#ifndef VRQ_K1R16
+#define VRQ_K1R16 1
+#endif
+#if VRQ_K1R16
+#define K1R_MB2(MODE) hamming_mfma_rows16_kernel<MODE>
+#else
+#define K1R_MB2(MODE) hamming_mfma_rows_lean_kernel<MODE, 2>
+#endif
 int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const uint8_t* q, int nq, int K,
                      uint8_t* ws, hipStream_t s, int flags) {
   constexpr int ALL = VRQ_SCAN_STAGE_PREFIX | VRQ_SCAN_STAGE_MATRIX | VRQ_SCAN_STAGE_RECHECK | VRQ_SCAN_STAGE_SUFFIX;
@@ -1795,7 +2094,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   if ((st & VRQ_SCAN_STAGE_PREFIX) && p.rows_sample) {  // dense sample pass (K1r) + per-query thresholds
     // (rows_sample implies MB <= 2: the MB = 1 instance fills the unreachable MB = 4 slot)
     if (p.mb > 2) return VRQ_EUNSUPPORTED;
-    rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, hamming_mfma_rows_lean_kernel<MFMA_SAMPLE, 2>,
+    rows_pass(hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, K1R_MB2(MFMA_SAMPLE),
               hamming_mfma_rows_kernel<MFMA_SAMPLE, 1>, none, none, none, p.sample_chunks, p.sample_chunk_rows,
               p.sample_stride, p.sample_tile_stride, dv, p.dvcols);
     VRQ_LAUNCH_CHECK();
@@ -1813,7 +2112,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
     VRQ_LAUNCH_CHECK();
   }
   if ((st & VRQ_SCAN_STAGE_MATRIX) && p.rows) {
-    rows_pass(hamming_mfma_rows_kernel<MFMA_MAIN, 1>, hamming_mfma_rows_lean_kernel<MFMA_MAIN, 2>,
+    rows_pass(hamming_mfma_rows_kernel<MFMA_MAIN, 1>, K1R_MB2(MFMA_MAIN),
               hamming_mfma_rows_kernel<MFMA_MAIN, 4>, (const int32_t*)(sampled ? tau_s : tau_p), none, none,
               p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
@@ -1834,7 +2133,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                        nq, rerun, qbflag, p.qpb);
     VRQ_LAUNCH_CHECK();
     if (p.rows)
-      rows_pass(hamming_mfma_rows_kernel<MFMA_RERUN, 1>, hamming_mfma_rows_lean_kernel<MFMA_RERUN, 2>,
+      rows_pass(hamming_mfma_rows_kernel<MFMA_RERUN, 1>, K1R_MB2(MFMA_RERUN),
                 hamming_mfma_rows_kernel<MFMA_RERUN, 4>, (const int32_t*)tau_p, (const int32_t*)rerun,
                 (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
                 (int64_t)0);

@@ -30,9 +30,9 @@
 //    K-list per query, exactly in every case (overflow -> exact rescan).
 #include <stdlib.h>
 
-#include "mfma_common.h"
-#include "vrq_internal.h"
-#include "vrq_scan.h"
+#include "../../../vectorragquantization_amd/csrc/mfma_common.h"
+#include "../../../vectorragquantization_amd/csrc/vrq_internal.h"
+#include "../../../vectorragquantization_amd/csrc/vrq_scan.h"
 
 namespace vrq {
 
@@ -170,22 +170,20 @@ constexpr int k1m_wait(int gi, int mb, bool dense) {
 // statistics sample_select_kernel takes over these minima are >= those over every sample distance:
 // tau_p (K-th + 1) still has K distinct rows below it, and tau_s only admits more rows (the recheck
 // proves it per query either way).
-// The minima are kept in float: v = pc(r) - 2 acc is one v_fma_f32 and the fold one v_min_f32 per
-// register (exact: integers far below 2^24), a row past the chunk end contributes +inf.
+constexpr int DMIN_NONE = 0x7000;
 template <bool ON, int MB>
 struct DenseMin {  // the sample pass's lane minima (ON); empty in the thresholded passes
-  float v[MB][16];
+  int v[MB][16];
   __device__ __forceinline__ DenseMin() {
 #pragma unroll
     for (int m = 0; m < MB; ++m)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) v[m][g] = __builtin_inff();
+      for (int g = 0; g < 16; ++g) v[m][g] = DMIN_NONE;
   }
   // v = pc(r) - 2 <q, r> of the 16 registers of M-block m (a row past the chunk end: no value)
   __device__ __forceinline__ void fold(const v16f& a, int m, int pc, bool ok) {
-    const float pcf = ok ? (float)pc : __builtin_inff();
 #pragma unroll
-    for (int g = 0; g < 16; ++g) v[m][g] = fminf(v[m][g], fmaf(-2.0f, a[g], pcf));
+    for (int g = 0; g < 16; ++g) v[m][g] = min(v[m][g], ok ? pc - (int)(2.0f * a[g]) : DMIN_NONE);
   }
   // -> dv[q][col] as u16 (v + 1024; 0xFFFF: no row), col = chunk * 32 + lane row
   __device__ __forceinline__ void out(uint16_t* __restrict__ dv, int64_t dv_stride, int64_t col, int qbase, int h,
@@ -195,8 +193,7 @@ struct DenseMin {  // the sample pass's lane minima (ON); empty in the threshold
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int q = qbase + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
-        if (q < nq)
-          dv[(int64_t)q * dv_stride + col] = v[m][g] == __builtin_inff() ? (uint16_t)0xFFFF : (uint16_t)((int)v[m][g] + 1024);
+        if (q < nq) dv[(int64_t)q * dv_stride + col] = v[m][g] >= DMIN_NONE ? (uint16_t)0xFFFF : (uint16_t)(v[m][g] + 1024);
       }
   }
 };

@@ -14,6 +14,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 // compile-time loop: f(integral_constant<int, I>) for I in [I0, N) -- every index a constant,
 // so register arrays indexed by it stay in registers (a #pragma unroll may give up)
