@@ -51,15 +51,20 @@ constexpr int STG = 512;                    // per-wave staged hit entries (u32)
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
 // M-blocks (32 queries each) per wave: MB = 4 for large batches (512 queries per workgroup, each
 // B fragment feeds 4 MFMAs), MB = 2 below (256 per workgroup)
-template <int MB>
+template <int MB, int NW = MWAVES>
 struct MfmaShape {
   static constexpr int QPW = 32 * MB;                 // queries per wave
-  static constexpr int QPB = MWAVES * QPW;            // queries per workgroup
+  static constexpr int QPB = NW * QPW;                // queries per workgroup
   static constexpr int SMEM =
-      NPK * PKT + NUB * UBT + NUB * RT * 4 + MWAVES * QPW * 8 + MWAVES * (STG + 1) * 4 + MWAVES * MB * 128;
+      NPK * PKT + NUB * UBT + NUB * RT * 4 + NW * QPW * 8 + NW * (STG + 1) * 4 + NW * MB * 128;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
 };
 constexpr int kMbLarge = 4, kMbSmall = 2;
+// large batches: 8 waves of MB = 2 (two per SIMD, sharing each unpacked tile) instead of 4 waves of MB = 4
+#ifndef VRQ_K1M_NW8
+#define VRQ_K1M_NW8 1
+#endif
+constexpr int kNwLarge = VRQ_K1M_NW8 ? 8 : 4, kMbLargeWave = VRQ_K1M_NW8 ? 2 : 4;
 constexpr int kMbLargeMinQueries = 512;     // batches of >= 512 queries take the MB = 4 kernel
 constexpr int kRowsMaxQueries = 128;        // batches of <= 128 queries take the row-split kernel K1r
 
@@ -146,16 +151,26 @@ enum { MFMA_MAIN = 0, MFMA_SAMPLE = 1, MFMA_RERUN = 2 };
 // accumulator-seed reads, the two hit-flush steps).  Groups gi < BAHEAD read tiles the previous
 // iteration's lgkmcnt(0) retired: their wait counts this iteration's operations so far.  Capped at 15
 // (the counter's range; a smaller count only waits longer).
-constexpr int k1m_pre(int g) { return ((g & 7) == 1 ? 1 : 0) + (g == 12 ? 2 : 0); }
-constexpr int k1m_post(int g, int mb, bool dense) {
-  const int j = g & 15;
-  return ((g & 7) == 6 ? 2 : 0) + (g == 28 ? 1 : 0) + (!dense && j >= 4 + mb && j < 4 + 2 * mb ? 4 : 0) +
-         (!dense && g == 20 + mb ? 1 : 0) + (!dense && g == 24 + mb ? 1 : 0);
+#ifndef VRQ_K1M_EXACT_WAIT
+#define VRQ_K1M_EXACT_WAIT 1
+#endif
+// (nw waves per workgroup: 16 / nw unpack units per wave, read in groups 8u + 1 and written in 8u + 6;
+// the row popcounts' packed pieces: two reads per lane at nw = 4, one at nw = 8)
+constexpr int k1m_pre(int g, int nw) {
+  return ((g & 7) == 1 && (g >> 3) < 16 / nw ? 1 : 0) + (g == 12 ? (nw == 4 ? 2 : 1) : 0);
 }
-constexpr int k1m_wait(int gi, int mb, bool dense) {
+constexpr int k1m_post(int g, int mb, bool dense, int nw) {
+  const int j = g & 15;
+  return ((g & 7) == 6 && (g >> 3) < 16 / nw ? 2 : 0) + (g == 28 ? 1 : 0) +
+         (!dense && j >= 4 + mb && j < 4 + 2 * mb ? 4 : 0) + (!dense && g == 20 + mb ? 1 : 0) +
+         (!dense && g == 24 + mb ? 1 : 0);
+}
+constexpr int k1m_wait(int gi, int mb, bool dense, int nw) {
+  if (!VRQ_K1M_EXACT_WAIT) return BAHEAD;
   const int g0 = gi - BAHEAD;
-  int n = 1 + k1m_pre(gi);  // this group's B read and pre-wait reads
-  for (int g = g0 < 0 ? 0 : g0; g < gi; ++g) n += (g == g0 ? 0 : 1) + k1m_pre(g) + k1m_post(g, mb, dense);
+  int n = 1 + k1m_pre(gi, nw);  // this group's B read and pre-wait reads
+  for (int g = g0 < 0 ? 0 : g0; g < gi; ++g)
+    n += (g == g0 ? 0 : 1) + k1m_pre(g, nw) + k1m_post(g, mb, dense, nw);
   return n < 15 ? n : 15;
 }
 
@@ -201,23 +216,26 @@ struct DenseMin<false, MB> {
   __device__ __forceinline__ void fold(const v16f&, int, int, bool) {}
   __device__ __forceinline__ void out(uint16_t*, int64_t, int64_t, int, int, int) const {}
 };
-template <int MODE, int MB>
-__global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
+template <int MODE, int MB, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void hamming_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, int nqb,
     const int32_t* __restrict__ rerun,
     const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv, int64_t dv_stride) {
   constexpr bool DENSE = MODE == MFMA_SAMPLE;
-  constexpr int QPW = MfmaShape<MB>::QPW, QPB = MfmaShape<MB>::QPB;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[MfmaShape<MB>::SMEM];
+  constexpr int QPW = MfmaShape<MB, NW>::QPW, QPB = MfmaShape<MB, NW>::QPB;
+  // NW = 4: one wave per SIMD; NW = 8: two (MB = 2 each, the same 512 queries per workgroup)
+  constexpr int GPWk = (PKT / 1024) / NW;  // LDS-DMA pieces per wave per tile
+  constexpr int UPW = 16 / NW;             // unpack units (n-block, 16-B piece) per wave per tile
+  __shared__ __attribute__((aligned(16))) uint8_t smem[MfmaShape<MB, NW>::SMEM];
   uint8_t* pk = smem;                                       // NPK packed tiles
   uint8_t* ub = smem + NPK * PKT;                           // NUB unpacked tiles
   int32_t* pcr = (int32_t*)(smem + NPK * PKT + NUB * UBT);  // NUB x 64 row popcounts
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int32_t* lcnt = pcr + NUB * RT + w * QPW;                 // this wave's list lengths
-  int32_t* tq = pcr + NUB * RT + MWAVES * QPW + w * QPW;    // this wave's tau'(q) = tau(q) - pc(q)
-  int32_t* stg = pcr + NUB * RT + 2 * MWAVES * QPW + w * (STG + 1);  // this wave's hit staging (+1 spare)
+  int32_t* tq = pcr + NUB * RT + NW * QPW + w * QPW;    // this wave's tau'(q) = tau(q) - pc(q)
+  int32_t* stg = pcr + NUB * RT + 2 * NW * QPW + w * (STG + 1);  // this wave's hit staging (+1 spare)
 
   const int l = lane_id();
   const int h = l >> 5, ri = l & 31;
@@ -242,13 +260,15 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   const int nrows = strided ? (int)chunk_rows : (int)(row1 - row0);
   const int ntiles = (nrows + RT - 1) / RT;
 
-  // LDS-DMA of packed tile t: this wave's GPW pieces of 64 x 16 B (lane -> (row, piece) through the
+  // LDS-DMA of packed tile t: this wave's GPWk pieces of 64 x 16 B (lane -> (row, piece) through the
   // swizzle).  Whole tiles take a uniform base + a fixed per-lane offset; the last partial tile
   // clamps each row to the chunk's last row.
+  // (bounds sized for NW = 4, first GPWk / UPW used: a template-dependent bound on an array the lambdas
+  // capture makes clang drop the host-side kernel stub without a diagnostic)
   uint32_t doff[GPW];
 #pragma unroll
-  for (int i = 0; i < GPW; ++i) {
-    const int p = (w * GPW + i) * 64 + l;
+  for (int i = 0; i < GPWk; ++i) {
+    const int p = (w * GPWk + i) * 64 + l;
     const int r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
     doff[i] = (uint32_t)(r * 128 + c * 16);
   }
@@ -258,16 +278,16 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     if (tr0 + RT <= row1) {
       const uint8_t* base = codes + tr0 * 128;
 #pragma unroll
-      for (int i = 0; i < GPW; ++i)
-        __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + (w * GPW + i) * 1024),
+      for (int i = 0; i < GPWk; ++i)
+        __builtin_amdgcn_global_load_lds(base + doff[i], (__attribute__((address_space(3))) void*)(buf + (w * GPWk + i) * 1024),
                                          16, 0, 0);
     } else {
 #pragma unroll
-      for (int i = 0; i < GPW; ++i) {
+      for (int i = 0; i < GPWk; ++i) {
         int64_t row = tr0 + (doff[i] >> 7);
         row = row < row1 ? row : row1 - 1;
         __builtin_amdgcn_global_load_lds(codes + row * 128 + (doff[i] & 127),
-                                         (__attribute__((address_space(3))) void*)(buf + (w * GPW + i) * 1024), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(buf + (w * GPWk + i) * 1024), 16, 0, 0);
       }
     }
   };
@@ -279,25 +299,26 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // [n-block][k-step][lane][16 B]: group g = 16*nblk + s.
   uint32_t usrc[4], udst[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int unit = 4 * w + u, nblk = unit >> 3, p = unit & 7;
+  for (int u = 0; u < UPW; ++u) {
+    const int unit = UPW * w + u, nblk = unit >> 3, p = unit & 7;
     const int r = nblk * 32 + ri;
     usrc[u] = (uint32_t)(pk_slot(r, p) * 16 + h * 8);
     udst[u] = (uint32_t)(((nblk * KS + 2 * p) * 64 + l) * 16);
   }
-  // row popcounts: tile rows 16w..16w+15, 4 lanes per row, 2 pieces each
-  const int pr = 16 * w + (l >> 2), pc0 = 2 * (l & 3);
+  // row popcounts: tile rows (64 / NW) w .., NW lanes per row, 8 / NW pieces each
+  const int pr = (64 / NW) * w + l / NW, pc0 = (8 / NW) * (l % NW);
   const uint32_t psrc0 = (uint32_t)(pk_slot(pr, pc0) * 16), psrc1 = (uint32_t)(pk_slot(pr, pc0 + 1) * 16);
   auto unpack_write = [&](const v2i& v, int u, uint32_t ubuf) __attribute__((always_inline)) {
     lds_write128(ubuf + udst[u], unpack_row32((uint32_t)v.x));
     lds_write128(ubuf + udst[u] + 1024, unpack_row32((uint32_t)v.y));
   };
   auto rowpc_write = [&](const v4i& a, const v4i& c, uint32_t pbuf) __attribute__((always_inline)) {
-    int pc = (__popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w)) +
-             (__popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w));
+    int pc = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w);
+    if constexpr (NW == 4) pc += __popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w);
     pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
     pc += __builtin_amdgcn_update_dpp(0, pc, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-    if ((l & 3) == 0) lds_write32(pbuf + (uint32_t)(pr * 4), pc);
+    if constexpr (NW == 8) pc += __builtin_amdgcn_update_dpp(0, pc, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    if ((l % NW) == 0) lds_write32(pbuf + (uint32_t)(pr * 4), pc);
   };
 
   // ---- prologue: DMA tiles 0..NPK-1, A fragments + thresholds, unpack tiles 0 and 1 ----
@@ -333,7 +354,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // a candidate iff pc(r) - 2<q,r> < tau'  <=>  acc > pc(r)/2.  The seeds of M-block m stay in LDS
   // (sd: [m][h][g] floats, 64 B per lane half: broadcast reads) and are loaded into the
   // accumulators of an n-block right after that block's epilogue.
-  float* sd = reinterpret_cast<float*>(pcr + NUB * RT + 2 * MWAVES * QPW + MWAVES * (STG + 1)) + w * MB * 32;
+  float* sd = reinterpret_cast<float*>(pcr + NUB * RT + 2 * NW * QPW + NW * (STG + 1)) + w * MB * 32;
 #pragma unroll
   for (int m = 0; m < MB; ++m)
     if (l < 32) {  // lane l writes [m][h = l >> 4][g = l & 15]
@@ -357,24 +378,24 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // at most k tiles' DMA still in flight (k <= NPK - 2; wave-uniform k)
   auto wait_tiles = [&](int k) __attribute__((always_inline)) {
     if (k <= 0) wait_vm<0>();
-    else if (k == 1) wait_vm<GPW>();
-    else if (k == 2) wait_vm<2 * GPW>();
-    else if (k == 3) wait_vm<3 * GPW>();
-    else wait_vm<4 * GPW>();
+    else if (k == 1) wait_vm<GPWk>();
+    else if (k == 2) wait_vm<2 * GPWk>();
+    else if (k == 3) wait_vm<3 * GPWk>();
+    else wait_vm<4 * GPWk>();
   };
   static_assert(NPK - 2 <= 4, "wait_tiles covers up to 4 tiles in flight");
   const int nissued = ntiles < NPK ? ntiles : NPK;
   wait_tiles(nissued - 2);
   barrier_all();  // packed tiles 0 and 1 visible to all waves
   {
-    v2i pv[8];
-    v4i pa[2], pb[2];
+    v2i pv[8] = {};
+    v4i pa[2], pb[2] = {};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) lds_read64(pv[4 * t + u], pk0 + (uint32_t)(t * PKT) + usrc[u]);
+      for (int u = 0; u < UPW; ++u) lds_read64(pv[4 * t + u], pk0 + (uint32_t)(t * PKT) + usrc[u]);
       lds_read128(pa[t], pk0 + (uint32_t)(t * PKT) + psrc0);
-      lds_read128(pb[t], pk0 + (uint32_t)(t * PKT) + psrc1);
+      if constexpr (NW == 4) lds_read128(pb[t], pk0 + (uint32_t)(t * PKT) + psrc1);
     }
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(pv[4]), "+v"(pv[5]), "+v"(pv[6]),
@@ -382,7 +403,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) unpack_write(pv[4 * t + u], u, ub0 + (uint32_t)(t * UBT));
+      for (int u = 0; u < UPW; ++u) unpack_write(pv[4 * t + u], u, ub0 + (uint32_t)(t * UBT));
       rowpc_write(pa[t], pb[t], pcr0 + (uint32_t)(t * RT * 4));
     }
   }
@@ -543,16 +564,16 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       else
         lds_read128_imm<(gi + BAHEAD - NG) * 1024>(ring[(gi + BAHEAD) & (NRING - 1)], bln);
       // packed reads of the unpack units (used 5 groups later) and of the row popcounts
-      if constexpr ((gi & 7) == 1) lds_read64(pv, pks + usrc[gi >> 3]);
+      if constexpr ((gi & 7) == 1 && (gi >> 3) < UPW) lds_read64(pv, pks + usrc[gi >> 3]);
       if constexpr (gi == 12) {
         lds_read128(pa, pks + psrc0);
-        lds_read128(pb, pks + psrc1);
+        if constexpr (NW == 4) lds_read128(pb, pks + psrc1);
       }
       // every LDS operation issued up to the B read of group gi - BAHEAD has completed (k1m_wait): the
       // fragment of this group, the packed unit read 5 groups ago, the popcounts, the seeds
       asm volatile("s_waitcnt lgkmcnt(%7)"
                    : "+v"(ring[gi & (NRING - 1)]), "+v"(pv), "+v"(pcv[0]), "+v"(pcv[1]), "+v"(pa), "+v"(pb), "+v"(fe)
-                   : "n"(k1m_wait(gi, MB, DENSE))
+                   : "n"(k1m_wait(gi, MB, DENSE, NW))
                    : "memory");
       // The group's non-MFMA work is cut into four slots that sit between its MFMAs (slot k after
       // MFMA k; at MB = 2 slots 2k and 2k+1 after MFMA k): an in-order wave issues them while the
@@ -566,7 +587,7 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
       //   asynchronous hit flush (gi = 20+MB and 24+MB, slot 3)
       constexpr bool TEST = !DENSE && j >= 2 && j < 2 + MB;
       constexpr int tm = TEST ? j - 2 : 0;
-      constexpr bool UNPACK = (gi & 7) == 6;
+      constexpr bool UNPACK = (gi & 7) == 6 && (gi >> 3) < UPW;
       constexpr bool SEED = !DENSE && j >= 4 + MB && j < 4 + 2 * MB;
       constexpr int sm = SEED ? j - 4 - MB : 0;
       int e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, f0 = 0;
@@ -622,14 +643,17 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
             pc0 = __popc(pa.x) + __popc(pa.y) + __popc(pa.z) + __popc(pa.w);
             asm volatile("" ::"v"(pc0));
           } else if constexpr (k == 1) {
-            pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
-            asm volatile("" ::"v"(pc1));
+            if constexpr (NW == 4) {
+              pc1 = __popc(pb.x) + __popc(pb.y) + __popc(pb.z) + __popc(pb.w);
+              asm volatile("" ::"v"(pc1));
+            }
           } else if constexpr (k == 2) {
             pc0 = pc0 + pc1;
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
             asm volatile("" ::"v"(pc0));
           } else {
             pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+            if constexpr (NW == 8) pc0 += __builtin_amdgcn_update_dpp(0, pc0, 0x141, 0xf, 0xf, false);  // row_half_mirror
             // every lane of the quad writes the same sum (no exec-masked branch: the counted waits
             // above assume this write is issued on every path)
             lds_write32(pcr0 + (uint32_t)(((t + 2) % NUB) * RT * 4 + pr * 4), pc0);
@@ -1764,11 +1788,11 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   int32_t* qbflag = (int32_t*)(ws + p.off_tau + 3 * qa);
   const bool sampled = p.j < K;
   const int32_t* none = nullptr;
-  // the MB = 4 or MB = 2 instance of a pass
+  // the large-batch (512 queries per workgroup) or MB = 2 (256) instance of a pass
   auto pass = [&](auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd, int32_t* cc, int64_t crows,
                   int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d, int64_t dstride) {
     if (p.mb == kMbLarge)
-      hipLaunchKernelGGL(kern4, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
+      hipLaunchKernelGGL(kern4, dim3(grid), dim3(kNwLarge * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
                          crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
     else
       hipLaunchKernelGGL(kern2, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
@@ -1799,7 +1823,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                        tau_s, tau_p, rerun, qbflag, p.nqb);
     VRQ_LAUNCH_CHECK();
   } else if (st & VRQ_SCAN_STAGE_PREFIX) {  // dense sample pass + per-query thresholds
-    hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
+    hipLaunchKernelGGL((hamming_mfma_kernel<MFMA_SAMPLE, kMbSmall, MWAVES>), dim3(p.sample_chunks * p.nqb_s), dim3(MWAVES * 64),
                        0, s, codes, n, (int64_t)0, q, nq, none, (uint64_t*)nullptr, (int32_t*)nullptr, 0,
                        p.sample_chunk_rows, p.sample_stride, p.sample_tile_stride, p.sample_chunks, p.nqb_s, none,
                        none, dv, p.dvcols);
@@ -1819,7 +1843,8 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
 #else
     uint16_t* mdv = nullptr;
 #endif
-    pass(hamming_mfma_kernel<MFMA_MAIN, kMbLarge>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
+    pass(hamming_mfma_kernel<MFMA_MAIN, kMbLargeWave, kNwLarge>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall, MWAVES>,
+         p.nchunks * p.nqb,
          (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
          mdv, (int64_t)0);
     VRQ_LAUNCH_CHECK();
@@ -1835,7 +1860,8 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                 (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
                 (int64_t)0);
     else
-      pass(hamming_mfma_kernel<MFMA_RERUN, kMbLarge>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
+      pass(hamming_mfma_kernel<MFMA_RERUN, kMbLargeWave, kNwLarge>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall, MWAVES>,
+           p.nchunks * p.nqb,
            (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
            (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();

@@ -47,13 +47,6 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {
   return (uint32_t)__shfl_xor((int)v, m, WAVE);
 }
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  uint32_t lo = shfl_xor_u32((uint32_t)v, m), hi = shfl_xor_u32((uint32_t)(v >> 32), m);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
-  return __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(v), m));
-}
 
 // Wave butterflies without the LDS crossbar.  A __shfl_xor is a ds_bpermute round trip (~100+ cycles
 // on the wave's critical path, twice for 64-bit values); here lane l meets lane l ^ M through
@@ -63,11 +56,7 @@ __device__ __forceinline__ double shfl_xor_f64(double v, int m) {
 //             establish for a commutative combine;
 //   M = 16, 32: v_permlane16/32_swap, which hand every lane both values of its pair.
 // Each lane then computes OP(own, partner) or OP(partner, own); for a commutative OP that is the
-// value the __shfl_xor butterfly computes, bit for bit.  VRQ_WAVE_SUM_DPP=0 (probe builds) keeps
-// the __shfl_xor form.
-#ifndef VRQ_WAVE_SUM_DPP
-#define VRQ_WAVE_SUM_DPP 1
-#endif
+// value the __shfl_xor butterfly computes, bit for bit.
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
@@ -107,22 +96,10 @@ __device__ __forceinline__ T wave_allreduce64(T v, OP op) {
 
 // f64 wave sum (butterfly; identical result in every lane)
 __device__ __forceinline__ double wave_sum_f64(double v) {
-  if constexpr (VRQ_WAVE_SUM_DPP) {
-    return wave_allreduce64(v, [](double a, double b) { return a + b; });
-  } else {
-#pragma unroll
-    for (int m = 1; m < WAVE; m <<= 1) v += shfl_xor_f64(v, m);
-    return v;
-  }
+  return wave_allreduce64(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-  if constexpr (VRQ_WAVE_SUM_DPP) {
-    return wave_allreduce64(v, [](int64_t a, int64_t b) { return a + b; });
-  } else {
-#pragma unroll
-    for (int m = 1; m < WAVE; m <<= 1) v += (int64_t)shfl_xor_u64((uint64_t)v, m);
-    return v;
-  }
+  return wave_allreduce64(v, [](int64_t a, int64_t b) { return a + b; });
 }
 
 // Sortable 64-bit image of a double for DESCENDING order: larger double -> smaller key.
