@@ -142,8 +142,8 @@ int vrq_search3_finish(const uint8_t* codes, const int8_t* x8, const double* nor
 #define VRQ_SCAN_KIND_MFMA 1
 int vrq_scan_kind(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, int64_t* prefix_rows);
 /* Host-only planning introspection of the matrix-core scan (no reference counterpart; tests and
- * tools): info i64[12] = row-split kernel (1) or shared-tile kernel (0), M-blocks (32 queries) per
- * wave, chunk rows, chunks, per-(query, chunk) list capacity, workspace offsets of
+ * tools): info i64[12] = row-split kernel K1r (1), shared-tile kernel K1m (0) or row-set kernel K1s (2,
+ * large batches of short passes), M-blocks (32 queries) per wave (K1s: 4, its 512-query blocks), chunk rows, chunks, per-(query, chunk) list capacity, workspace offsets of
  * the candidate lists (u64 keys (v + 1025) << 40 | row, v = dist - tau), of the list lengths (i32
  * [nq][chunks]) and of tau_s / tau_p / rerun (i32 [nq] each, 256-B aligned), sample rows, sampled
  * order j, offset of the sorted K-lists, workspace bytes.  VRQ_EUNSUPPORTED when the shape takes the

@@ -182,6 +182,19 @@ def test_no_copies_of_inflight_lds_reads(tmp_path):
     assert not bad, [f"{k}: {i} <- {ld}" for k, i, ld in bad[:4]]
 
 
+@pytest.mark.parametrize("n,nq,kernel", [(1_000_000, 1024, 2), (4_194_304, 1024, 2), (4_194_305, 1024, 0),
+                                         (1_000_000, 511, 0), (100_000_000, 1024, 0), (1_000_000, 64, 1)])
+def test_scan_plan_picks_k1s_for_short_large_batch_passes(n, nq, kernel):
+    """Batches of >= 512 queries run K1s (row sets resident, queries streamed; kind 2) while the pass has
+    at most 2^32 (query, row) pairs and K1m's MB = 4 instance (kind 0) above; both in 512-query blocks."""
+    lib = N.load()
+    info = np.zeros(12, np.int64)
+    N.check(lib.vrq_scan_plan(n, 1024, nq, 100, 0, info.ctypes.data), "plan")
+    assert int(info[0]) == kernel
+    if nq >= 512:
+        assert int(info[1]) == 4
+
+
 @pytest.mark.parametrize("nq,rows_kernel,mb", [(1, 1, 1), (32, 1, 1), (33, 1, 2), (64, 1, 2), (65, 1, 4),
                                                (128, 1, 4), (129, 0, 2), (1024, 0, 4)])
 def test_scan_plan_picks_the_k1r_instance(nq, rows_kernel, mb):

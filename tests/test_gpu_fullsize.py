@@ -5,7 +5,7 @@
   small-batch scan (K1r) at nq = 1, 8 and 64, K = 100, against the C restatement of FAISS
   hammings_knn_hc over every row.  Every (dist, row) of the top-K must be identical.
 * Config 2 -- the 3-phase search over 1M rows with the full nq = 1024 batch, i.e. the MB = 4 instance
-  of the shared-tile matrix-core scan (K1m) the config-2 bench runs: 32 sampled queries against the
+  of the large-batch matrix-core scan (K1s) the config-2 bench runs: 32 sampled queries against the
   FAISS restatement (Phase I, every (dist, row) of the top-K) and the reference Phases II/III
   (CohereEnhancedVectorDB.py:267-322).
 * Config 5 -- exhaustive Phase-II / Phase-III top-k over 10M x 1024 rows, nq = 1024 (four 256-query
@@ -132,7 +132,7 @@ def test_config2_1m_batch_1024_vs_reference(dev, oracle_lib):
     lib = N.load()
     info = np.zeros(12, np.int64)
     N.check(lib.vrq_scan_plan(n, 1024, nq, K, 0, info.ctypes.data), "plan")
-    assert int(info[0]) == 0 and int(info[1]) == 4, info[:2]  # K1m, 4 M-blocks per wave
+    assert int(info[0]) == 2 and int(info[1]) == 4, info[:2]  # K1s, 512-query blocks
     sh = synth.make_corpus(n, device=dev)
     codes, x8, norms = sh["codes"], sh["x8"], sh["norms"]
     qf, qb, _ = synth.make_queries(n, nq, device=dev)

@@ -9,7 +9,7 @@ the true value, and every list against the exact set of rows it must hold:
   PREFIX + MATRIX (+ RECHECK) stages, list (q, chunk) must be exactly the rows r of the chunk with
   dist(q, r) < tau(q) (tau = the threshold the pass ran with: tau_s, or tau_p for re-run queries), each
   once, with its exact distance in the key.  Every K1r instance (MB = 1, the lean MB = 2, MB = 4) and
-  both K1m instances (MB = 2, MB = 4), 4M+ uniform rows (ragged: the last tile is partial).
+  both K1m instances (MB = 2, MB = 4) and K1s, 4M+ uniform rows (ragged: the last tile is partial).
 * The dense sample pass (PREFIX): every u16 lane minimum equals min(dist - pc(q)) + 1024 over the
   sample rows that lane holds.
 * K5 (gemm_topk.hip, CohereEnhancedVectorDB.py:283-293 / :302-318 scored against every row): after the
@@ -89,8 +89,8 @@ def _scan_stages(codes, qb, K, stages):
 
 
 # (nq, instance): K1r MB = 1 (<= 32 queries), the lean MB = 2 (33..64), MB = 4 (65..128); K1m MB = 2
-# (129..511), MB = 4 (>= 512)
-SCAN_CASES = [(8, (1, 1)), (40, (1, 2)), (64, (1, 2)), (128, (1, 4)), (256, (0, 2)), (1024, (0, 4))]
+# (129..511); >= 512: K1s (kind 2) up to 2^32 (query, row) pairs per pass, K1m MB = 4 above
+SCAN_CASES = [(8, (1, 1)), (40, (1, 2)), (64, (1, 2)), (128, (1, 4)), (256, (0, 2)), (1024, (2, 4)), (1536, (0, 4))]
 
 
 @pytest.mark.parametrize("nq,inst", SCAN_CASES)

@@ -87,7 +87,7 @@ def test_mfma_auto_selection_in_hamming_topk(dev, oracle_lib):
     assert np.array_equal(D0, D1) and np.array_equal(I0 * 3 + 1, L1)
 
 
-@pytest.mark.parametrize("nq", [8, 40, 64])          # K1r MB = 1 and the lean MB = 2 kernel
+@pytest.mark.parametrize("nq", [8, 40, 64, 600])     # K1r MB = 1, the lean MB = 2 kernel; K1s
 def test_mfma_heavy_ties(dev, oracle_lib, nq):
     rng = np.random.default_rng(11)
     base = rng.integers(0, 256, (25, 128), dtype=np.uint8)
@@ -100,13 +100,14 @@ def test_mfma_heavy_ties(dev, oracle_lib, nq):
         assert np.array_equal(I0 + 5_000_000, I1)
 
 
-def test_mfma_candidate_overflow_exact_rescan(dev, oracle_lib):
+@pytest.mark.parametrize("nq", [130, 600])             # K1m MB = 2; K1s (512-query blocks)
+def test_mfma_candidate_overflow_exact_rescan(dev, oracle_lib, nq):
     """Query 0's neighbours fill rows [S, n): far more rows beat its threshold than a candidate
     list holds, so its lists overflow and the corpus is rescanned exactly.  Those rows hold 50
     exact copies (dist 0) and otherwise rows at dist exactly 3, so with K = 100 the answer is
     the 50 copies plus the FIRST 50 dist-3 rows in row order."""
     rng = np.random.default_rng(9)
-    n, nq, K = 100_000, 130, 100
+    n, K = 100_000, 100
     S = 32_768
     codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     qb = rng.integers(0, 256, (nq, 128), dtype=np.uint8)
@@ -170,7 +171,7 @@ def test_mfma_and_valu_three_phase_identical(dev):
         assert np.array_equal(a, b, equal_nan=True) and np.array_equal(a, c, equal_nan=True)
 
 
-@pytest.mark.parametrize("nq", [200, 64, 40])      # K1m MB = 2; the lean MB = 2 K1r (full and partial)
+@pytest.mark.parametrize("nq", [200, 64, 40, 600])  # K1m MB = 2; the lean MB = 2 K1r (full and partial); K1s
 def test_mfma_hit_staging_overflow(dev, oracle_lib, nq):
     """Up to 64 queries (one wave's worth) and the whole suffix clustered around one code: every tile
     gives a wave thousands of hits, more than its LDS staging holds, so the lists are marked overflowed
@@ -206,7 +207,7 @@ def _sample_rows(n, nq):
     return (np.arange(tiles)[:, None] * ts + np.arange(64)[None, :]).reshape(-1)
 
 
-@pytest.mark.parametrize("nq", [300, 100, 50])
+@pytest.mark.parametrize("nq", [300, 100, 50, 600])
 def test_mfma_sampled_threshold_rerun(dev, oracle_lib, nq):
     """The thresholded pass runs with the sampled tau_s = d_(j)+1 (j < K) of the dense sample.
     Queries 0 and nq - 10 (two different 256-query blocks at nq = 300; the one block of the

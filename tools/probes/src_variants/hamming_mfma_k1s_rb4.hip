@@ -769,28 +769,21 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 //     positions taken from the workgroup's per-query LDS counters (the four waves share the chunk).
 // The lists, their keys and the suffix merge are K1m's, so the pass is a drop-in for K1m's MB = 4
 // instance (same launch geometry: one workgroup per (chunk, 512-query block)).
-// K1s takes the large-batch pass up to this many (query, row) pairs per launch (1M rows x 1024 queries:
-// 0.34 vs 0.39 ms, config-2 step 0.538 vs 0.583 ms; 4M: 1.25 vs 1.36 ms).  Above, K1m: two waves per
-// SIMD each unpacking every query fragment cost more energy per MFMA than K1m's shared tile, and a long
-// pass is power-bound -- 100M x 1024 in the config-4 bench ran 32.8 ms on K1s vs 31.0 on K1m on one box
-// (K1s 2.22 GHz / 0.75 of the matrix cores busy vs K1m 2.37 GHz / 0.71; profiles/r5_k1s_ab.jsonl).
-constexpr double kSwapMaxPairs = 4294967296.0;
-constexpr int SRB = 2;          // row blocks of 32 rows per row set
-constexpr int SNW = 8;          // waves per workgroup (two per SIMD)
+constexpr int SRB = 4;          // row blocks of 32 rows per row set
 constexpr int SRS = SRB * 32;   // rows per row set (128)
 constexpr int SQPB = 512;       // queries per workgroup (16 blocks of 32)
 struct SwapShape {
   static constexpr int QBYTES = SQPB * 128;          // packed queries (swizzled 16-B pieces)
   static constexpr int RBYTES = SRS * 128;           // one wave's row staging
-  static constexpr int SMEM = QBYTES + SNW * RBYTES + SQPB * 4 /* thr */ + SQPB * 4 /* list lengths */ +
-                              SNW * (STG + 1) * 4 + SNW * SRB * 32 * 4 /* seeds */;
+  static constexpr int SMEM = QBYTES + MWAVES * RBYTES + SQPB * 4 /* thr */ + SQPB * 4 /* list lengths */ +
+                              MWAVES * (STG + 1) * 4 + MWAVES * SRB * 32 * 4 /* seeds */;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
 };
 // staged hit entry of K1s (u32): (v + 1025) << 16 | query-in-workgroup << 7 | row in the row set
 constexpr int SENT_V_SHIFT = 16, SENT_Q_SHIFT = 7;
 
 template <int MODE>
-__global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
+__global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_swap_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
     int64_t chunk_rows, int64_t chunk_stride, int64_t tile_stride, int nchunks, int nqb,
@@ -801,10 +794,10 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* qpk = smem;
   uint8_t* rst = smem + SwapShape::QBYTES + w * SwapShape::RBYTES;  // this wave's row staging
-  float* thr = reinterpret_cast<float*>(smem + SwapShape::QBYTES + SNW * SwapShape::RBYTES);
+  float* thr = reinterpret_cast<float*>(smem + SwapShape::QBYTES + MWAVES * SwapShape::RBYTES);
   int32_t* lcnt = reinterpret_cast<int32_t*>(thr + SQPB);
   int32_t* stg = lcnt + SQPB + w * (STG + 1);
-  float* sdw = reinterpret_cast<float*>(lcnt + SQPB + SNW * (STG + 1)) + w * SRB * 32;
+  float* sdw = reinterpret_cast<float*>(lcnt + SQPB + MWAVES * (STG + 1)) + w * SRB * 32;
   const int l = lane_id();
   const int h = l >> 5, ri = l & 31;
   const int nb = gridDim.x, b = blockIdx.x;
@@ -822,17 +815,15 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const int nqv = nq - qbase < SQPB ? nq - qbase : SQPB;
   const int nqblk = (((nqv + 31) >> 5) + 1) & ~1;  // query blocks, run in pairs
 
-  // packed queries -> LDS: piece c (16 B) of query j at 16-B slot pk_slot(j, c) = j*8 + (c ^ ((j >> 1) & 7))
-  // (conflict-free ds_read_b128 for a lane per query: any 16-lane group of the read covers all 16
-  // columns of 16 B); thresholds
-  for (int p = threadIdx.x; p < SQPB * 8; p += SNW * 64) {
+  // packed queries -> LDS: piece c (16 B) of query j at 16-B slot j*8 + (c ^ (j & 7)); thresholds
+  for (int p = threadIdx.x; p < SQPB * 8; p += MWAVES * 64) {
     const int j = p >> 3, c = p & 7, q = qbase + j;
     const bool qok = q < nq && (!rerun || rerun[q]);
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (qok) v = reinterpret_cast<const uint4*>(queries + (int64_t)q * 128)[c];
-    reinterpret_cast<uint4*>(qpk)[pk_slot(j, c)] = v;
+    reinterpret_cast<uint4*>(qpk)[j * 8 + (c ^ (j & 7))] = v;
   }
-  for (int j = threadIdx.x; j < SQPB; j += SNW * 64) {
+  for (int j = threadIdx.x; j < SQPB; j += MWAVES * 64) {
     const int q = qbase + j;
     const bool qok = q < nq && (!rerun || rerun[q]);
     int pc = 0;
@@ -849,19 +840,18 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     lcnt[j] = 0;
   }
 
-  // LDS-DMA of row set rs into this wave's staging: SRS / 8 pieces of 64 x 16 B; 16-B slot i*64 + l holds
-  // piece c of row r = 8i + (l >> 3) with pk_slot(r, c) = i*64 + l, i.e. c = (l & 7) ^ ((r >> 1) & 7),
-  // where (r >> 1) & 7 = (4 (i & 1) + (l >> 4)) & 7: one column per parity of i.  Rows past the chunk
-  // are clamped to its last row (their seeds mask them).
-  const int dcol0 = ((l & 7) ^ ((l >> 4) & 7)) * 16, dcol1 = ((l & 7) ^ ((4 + (l >> 4)) & 7)) * 16;
-  const int dlane0 = (l >> 3) * 128 + dcol0, dlane1 = (l >> 3) * 128 + dcol1;
+  // LDS-DMA of row set rs into this wave's staging: 16 pieces of 64 x 16 B; 16-B slot i*64 + l holds
+  // piece c = (l & 7) ^ ((l >> 3) & 7) of row 8i + (l >> 3) (the slot swizzle r*8 + (c ^ (r & 7))).
+  // Rows past the chunk are clamped to its last row (their seeds mask them).
+  const int dcol = ((l & 7) ^ ((l >> 3) & 7)) * 16;
+  const int dlane = (l >> 3) * 128 + dcol;
   auto issue = [&](int rs) __attribute__((always_inline)) {
     const int64_t r0 = row0 + (int64_t)rs * SRS;
     if (r0 + SRS <= row1) {
-      const uint8_t* base = codes + r0 * 128;
+      const uint8_t* base = codes + r0 * 128 + dlane;
 #pragma unroll
       for (int i = 0; i < SRS / 8; ++i) {
-        const uint8_t* src = base + i * 1024 + ((i & 1) ? dlane1 : dlane0);
+        const uint8_t* src = base + i * 1024;
         uint8_t* dst = rst + i * 1024;
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -870,7 +860,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
       for (int i = 0; i < SRS / 8; ++i) {
         int64_t row = r0 + 8 * i + (l >> 3);
         row = row < row1 ? row : row1 - 1;
-        const uint8_t* src = codes + row * 128 + ((i & 1) ? dcol1 : dcol0);
+        const uint8_t* src = codes + row * 128 + dcol;
         uint8_t* dst = rst + i * 1024;
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -944,7 +934,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     }
   };
 
-  const int nmine = w < nrs ? (nrs - w + SNW - 1) / SNW : 0;  // this wave's row sets
+  const int nmine = w < nrs ? (nrs - w + MWAVES - 1) / MWAVES : 0;  // this wave's row sets
   if (nmine > 0) {
     v4i A[SRB][KS];  // [rb][s]: dword 16h + s of row 32rb + ri of the row set, as 32 e2m1 values
     // the row set's A fragments and seeds from the staging buffer (its DMA landed)
@@ -954,7 +944,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
         const int r = 32 * rb + ri;
         v4i p[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lds_read128(p[i], rst0 + (uint32_t)(pk_slot(r, 4 * h + i) * 16));
+        for (int i = 0; i < 4; ++i) lds_read128(p[i], rst0 + (uint32_t)((r * 8 + ((4 * h + i) ^ (r & 7))) * 16));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3])::"memory");
         int pc = 0;
 #pragma unroll
@@ -992,21 +982,21 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     auto read_qblock = [&](v4i (&wq)[4], int& thb, int qbi) __attribute__((always_inline)) {
       const int j = qbi * 32 + ri;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) lds_read128_inplace(wq[i], q0 + (uint32_t)(pk_slot(j, 4 * h + i) * 16));
+      for (int i = 0; i < 4; ++i) lds_read128_inplace(wq[i], q0 + (uint32_t)((j * 8 + ((4 * h + i) ^ (j & 7))) * 16));
       lds_read32_inplace(thb, thr0 + (uint32_t)(j * 4));
     };
 
     wait_vm<0>();
     rebuild(row0 + (int64_t)w * SRS);
-    if (nmine > 1) issue(w + SNW);
+    if (nmine > 1) issue(w + MWAVES);
     v16f acc[2][SRB];
     v4i wq[2][4] = {};
     int thb[2] = {};
     static_for<0, SRB>([&](auto RB) { acc[0][RB] = read_seed(RB); });
     read_qblock(wq[0], thb[0], 0);
     asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                   "+v"(wq[0][3]), "+v"(thb[0])::"memory");
+                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(wq[0][0]), "+v"(wq[0][1]),
+                   "+v"(wq[0][2]), "+v"(wq[0][3]), "+v"(thb[0])::"memory");
 #ifdef VRQ_K1S_DEBUG
     if (L == 0 && w == 0) {
 #pragma unroll
@@ -1027,10 +1017,10 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     auto qblock = [&](auto PAR, int qbi, bool last) __attribute__((always_inline)) {
       constexpr int c = decltype(PAR)::value;
       {  // retire the reads of the previous block (this block's operands; a no-op before the first)
-        static_assert(SRB == 2, "the wait names the two row blocks' accumulators");
+        static_assert(SRB == 4, "the wait names the four row blocks' accumulators");
         asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(acc[c][0]), "+v"(acc[c][1]), "+v"(wq[c][0]), "+v"(wq[c][1]), "+v"(wq[c][2]),
-                       "+v"(wq[c][3]), "+v"(thb[c])::"memory");
+                     : "+v"(acc[c][0]), "+v"(acc[c][1]), "+v"(acc[c][2]), "+v"(acc[c][3]), "+v"(wq[c][0]),
+                       "+v"(wq[c][1]), "+v"(wq[c][2]), "+v"(wq[c][3]), "+v"(thb[c])::"memory");
       }
       static_for<0, KS>([&](auto S) {
         constexpr int s = decltype(S)::value;
@@ -1092,20 +1082,20 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
       if (k + 1 < nmine) {  // switch to the next row set: its DMA landed; start the one after
         wait_vm<0>();
         asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                       "+v"(wq[0][3]), "+v"(thb[0])::"memory");
-        set_base = row0 + (int64_t)(w + SNW * (k + 1)) * SRS;
+                     : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(wq[0][0]),
+                       "+v"(wq[0][1]), "+v"(wq[0][2]), "+v"(wq[0][3]), "+v"(thb[0])::"memory");
+        set_base = row0 + (int64_t)(w + MWAVES * (k + 1)) * SRS;
         rebuild(set_base);
-        if (k + 2 < nmine) issue(w + SNW * (k + 2));
+        if (k + 2 < nmine) issue(w + MWAVES * (k + 2));
         static_for<0, SRB>([&](auto RB) { acc[0][RB] = read_seed(RB); });
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0][0]), "+v"(acc[0][1])::"memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3])::"memory");
       }
     }
     // the last block of the last row set
     {
       asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                     "+v"(wq[0][3]), "+v"(thb[0])::"memory");
+                   : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(wq[0][0]),
+                     "+v"(wq[0][1]), "+v"(wq[0][2]), "+v"(wq[0][3]), "+v"(thb[0])::"memory");
       const float th = __int_as_float(thb[1]);
       static_for<0, SRB>([&](auto RB) {
         const v16i x = __builtin_bit_cast(v16i, acc[1][RB]);
@@ -1119,7 +1109,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   }
   wait_lgkm0();
   __syncthreads();  // every wave's list appends done
-  for (int j = threadIdx.x; j < SQPB; j += SNW * 64) {
+  for (int j = threadIdx.x; j < SQPB; j += MWAVES * 64) {
     const int q = qbase + j;
     if (q < nq && (!rerun || rerun[q])) ccnt[(int64_t)q * nchunks + chunk] = lcnt[j];
   }
@@ -2056,16 +2046,11 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   p->mb = (em == 2 || em == 4) ? em : nq >= kMbLargeMinQueries ? kMbLarge : kMbSmall;
   p->qpb = p->mb == kMbLarge ? MfmaShape<kMbLarge>::QPB : MfmaShape<kMbSmall>::QPB;
   p->nqb = (nq + p->qpb - 1) / p->qpb;
-  // large batches: K1s (row sets resident, queries streamed) for passes of <= kSwapMaxPairs (query, row)
-  // pairs, K1m above (see kSwapMaxPairs)
-  static_assert(SQPB == MfmaShape<kMbLarge>::QPB, "K1s serves K1m's MB = 4 query blocks");
-  p->swap = p->mb == kMbLarge && (double)n * (double)nq <= kSwapMaxPairs;
   // small batches (nq <= 128): the row-split kernel K1r, all queries in every wave
   // (VRQ_MFMA_ROWS=0: probe-build override)
   p->rows = nq <= kRowsMaxQueries && tuning_int("VRQ_MFMA_ROWS", 1) != 0;
   int rows_occ = 1;  // K1r workgroups per CU of the chosen instance
   if (p->rows) {
-    p->swap = 0;
     p->mb = nq <= 32 ? 1 : nq <= 64 ? 2 : 4;
     p->qpb = kRowsMaxQueries;
     p->nqb = 1;
@@ -2151,13 +2136,9 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   const bool sampled = p.j < K;
   const int32_t* none = nullptr;
   // the MB = 4 or MB = 2 instance of a pass
-  auto pass = [&](auto kswap, auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd, int32_t* cc,
-                  int64_t crows, int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d,
-                  int64_t dstride) {
-    if (p.swap)
-      hipLaunchKernelGGL(kswap, dim3(grid), dim3(SNW * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
-                         crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
-    else if (p.mb == kMbLarge)
+  auto pass = [&](auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd, int32_t* cc, int64_t crows,
+                  int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d, int64_t dstride) {
+    if (p.mb == kMbLarge)
       hipLaunchKernelGGL(kern4, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
                          crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
     else
@@ -2209,8 +2190,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
 #else
     uint16_t* mdv = nullptr;
 #endif
-    pass(hamming_mfma_swap_kernel<MFMA_MAIN>, hamming_mfma_kernel<MFMA_MAIN, kMbLarge>,
-         hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
+    pass(hamming_mfma_swap_kernel<MFMA_MAIN>, hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
          (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
          mdv, (int64_t)0);
     VRQ_LAUNCH_CHECK();
@@ -2226,8 +2206,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                 (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
                 (int64_t)0);
     else
-      pass(hamming_mfma_swap_kernel<MFMA_RERUN>, hamming_mfma_kernel<MFMA_RERUN, kMbLarge>,
-           hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
+      pass(hamming_mfma_swap_kernel<MFMA_RERUN>, hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
            (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
            (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();

@@ -16,6 +16,9 @@ def short(name):
         mode = name.split("_kernel<", 1)[-1][:1]
         return {"1": "hamming_mfma_rows_kernel_sample", "2": "hamming_mfma_rows_kernel_rerun"}.get(
             mode, "hamming_mfma_rows_kernel")
+    if "hamming_mfma_swap" in name:  # K1s, the large-batch thresholded pass (MODE 0) and its re-run (2)
+        mode = name.split("_swap_kernel<", 1)[-1][:1]
+        return "hamming_mfma_kernel_rerun" if mode == "2" else "hamming_mfma_kernel"
     if "hamming_mfma" in name:  # template MODE: 0 thresholded pass, 1 dense sample pass, 2 re-run
         return {"1": "hamming_mfma_kernel_sample", "2": "hamming_mfma_kernel_rerun"}.get(
             name.split("hamming_mfma_kernel<", 1)[-1][:1], "hamming_mfma_kernel")

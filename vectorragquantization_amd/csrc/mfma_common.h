@@ -60,6 +60,9 @@ __device__ __forceinline__ void lds_read64(v2i& d, uint32_t a) {
 __device__ __forceinline__ void lds_read32(int& d, uint32_t a) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
+__device__ __forceinline__ void lds_read32_inplace(int& d, uint32_t a) {
+  asm volatile("ds_read_b32 %0, %1" : "+v"(d) : "v"(a) : "memory");
+}
 __device__ __forceinline__ void lds_write128(uint32_t a, const v4i& v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }

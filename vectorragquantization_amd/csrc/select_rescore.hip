@@ -640,7 +640,7 @@ int vrq_scan_plan(int64_t n, int32_t dim, int32_t nq, int32_t K, int32_t flags, 
   MfmaPlan p;
   const int rc = mfma_plan(n, nq, K, &p);
   if (rc != VRQ_OK) return rc;
-  info[0] = p.rows;
+  info[0] = p.rows ? 1 : p.swap ? 2 : 0;
   info[1] = p.mb;
   info[2] = p.chunk_rows;
   info[3] = p.nchunks;
