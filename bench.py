@@ -1110,10 +1110,16 @@ def run_3phase(a, world, rank, dev):
         rows_m = m - P.prefix_rows
         ops = 2048.0 * nq * rows_m
         ach = ops / (st["matrix"] * 1e-3) / 1e12
-        kern = K1R_MAIN if nq <= 128 else "hamming_mfma_kernel<0"
+        # large batches: K1s (hamming_mfma_swap_kernel, plan kind 2) or K1m (hamming_mfma_kernel), both
+        # summarised under "hamming_mfma_kernel" in the committed PMC summaries (tools/summarize_profile.py)
+        info = np.zeros(12, np.int64)
+        N.check(N.load().vrq_scan_plan(m, 1024, nq, K, P.flags, info.ctypes.data), "plan")
+        k1s = int(info[0]) == 2
+        kern = K1R_MAIN if nq <= 128 else ("hamming_mfma_kernel<0", "hamming_mfma_swap_kernel<0")
         roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
                 "frac": ach / MFMA_FP4_PEAK_TOPS, "traffic": pmc_traffic(tag, _kname(kern)),
-                "kernel": f"{_kname(kern)} (FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
+                "kernel": f"{'hamming_mfma_swap_kernel (K1s)' if k1s else _kname(kern)} "
+                          "(FP4 e2m1 MX MFMA 32x32x64, f32 accumulate)",
                 "kernel_ms": st["matrix"], "timing": "HIP events on the library's stream, this run",
                 "algorithmic_ops_per_launch": ops, "algorithmic_bytes_per_launch": rows_m * 128 + nq * 128,
                 "rows": rows_m,

@@ -965,12 +965,6 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
           asm volatile("" : "+a"(A[rb][s]));  // straight to the accumulator file
         }
         pc += __shfl_xor(pc, 32, 64);  // both halves of the row
-#ifdef VRQ_K1S_DEBUG
-        if (L == 0 && w == 0 && r0 == row0 && rb == 0) {
-          reinterpret_cast<uint32_t*>(dv)[l] = (uint32_t)pc;
-          reinterpret_cast<uint32_t*>(dv)[3072 + l] = (uint32_t)p[0][0];
-        }
-#endif
         // seed of block row ri at [rb][hh][g], ri = (g & 3) + 8 (g >> 2) + 4 hh: lane halves read 16 floats each
         const float sv = r0 + r < row1 ? 1024.0f - 0.5f * (float)pc : -4096.0f;
         if (h == 0)
@@ -1007,15 +1001,6 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
                    "+v"(wq[0][3]), "+v"(thb[0])::"memory");
-#ifdef VRQ_K1S_DEBUG
-    if (L == 0 && w == 0) {
-#pragma unroll
-      for (int g = 0; g < 16; ++g) reinterpret_cast<uint32_t*>(dv)[64 + l * 16 + g] = __float_as_uint(acc[0][0][g]);
-      reinterpret_cast<uint32_t*>(dv)[1088 + l] = (uint32_t)thb[0];
-      reinterpret_cast<uint32_t*>(dv)[1152 + l] = (uint32_t)wq[0][0][0];
-    }
-    bool dbg_done = false;
-#endif
 
     bool have_prev = false;      // an untested block in acc[1 - parity]
     int prev_qb = 0;             // its query block
@@ -1038,19 +1023,6 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
         static_for<0, SRB>([&](auto RB) { acc[c][RB] = mfma_fp4(A[RB][s], bq, acc[c][RB]); });
         if constexpr (s == 1) {
           if (have_prev) {
-#ifdef VRQ_K1S_DEBUG
-            if (L == 0 && w == 0 && !dbg_done) {
-              dbg_done = true;
-#pragma unroll
-              for (int g = 0; g < 16; ++g) reinterpret_cast<uint32_t*>(dv)[2048 + l * 16 + g] = __float_as_uint(acc[c ^ 1][0][g]);
-            }
-            if (L == 0 && w == 0 && prev_qb < 16) {
-#pragma unroll
-              for (int g = 0; g < 16; ++g)
-                reinterpret_cast<uint32_t*>(dv)[8192 + prev_qb * 1024 + l * 16 + g] = __float_as_uint(acc[c ^ 1][1][g]);
-              reinterpret_cast<uint32_t*>(dv)[8192 + 16384 + prev_qb * 64 + l] = (uint32_t)nst;
-            }
-#endif
             const float th = __int_as_float(thb[c ^ 1]);
             uint64_t hm[SRB], any = 0;
             static_for<0, SRB>([&](auto RB) {
@@ -2204,7 +2176,7 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
               p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr, (int64_t)0);
     VRQ_LAUNCH_CHECK();
   } else if (st & VRQ_SCAN_STAGE_MATRIX) {
-#if defined(VRQ_K1M_STAMPS) || defined(VRQ_K1S_DEBUG)
+#ifdef VRQ_K1M_STAMPS
     uint16_t* mdv = dv;
 #else
     uint16_t* mdv = nullptr;
