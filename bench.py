@@ -622,6 +622,11 @@ def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517)):
 
 
 def timed_loop(P, a, world, dev):
+    """W untimed warm-up steps, then EXACTLY K timed steps between barrier + synchronize (max over ranks).
+    The timed steps carry no per-stage events: each timing event record costs ~4.8 us of GPU time on
+    this stack (two consecutive records are that far apart), ~40 us per step at 8 records -- 7 % of a
+    config-2 step.  The per-stage breakdown (stage_ms) comes from K further, instrumented steps run
+    after the timed region."""
     for _ in range(a.warmup):
         P.step(False)
     torch.cuda.synchronize()
@@ -630,7 +635,7 @@ def timed_loop(P, a, world, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        P.step(True)
+        P.step(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -639,6 +644,9 @@ def timed_loop(P, a, world, dev):
         tt = torch.tensor([T], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
+    for _ in range(a.steps):  # per-stage HIP events (not timed)
+        P.step(True)
+    torch.cuda.synchronize()
     return T
 
 
@@ -855,9 +863,12 @@ def phase1_leg(dev, n, nqs, k, osb, steps, warmup, threads, cpu=True, scan="auto
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            P.step(True)
+            P.step(False)
         torch.cuda.synchronize()
         T = time.perf_counter() - t0
+        for _ in range(steps):  # per-stage HIP events, after the timed region (see timed_loop)
+            P.step(True)
+        torch.cuda.synchronize()
         st = P.stage_ms()
         mb = n * 128 + nq * 128
         kern = K1R_MAIN if P.kind == N.VRQ_SCAN_KIND_MFMA and nq <= 128 else \
@@ -867,7 +878,7 @@ def phase1_leg(dev, n, nqs, k, osb, steps, warmup, threads, cpu=True, scan="auto
         pt = {"nq": nq, "qps": nq * steps / T, "ms_per_step": T / steps * 1e3, "phase_ms": st,
               "kernel": _kname(kern), "kernel_ms": kms, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
               "algorithmic_bytes_per_launch": mb, "timing": f"HIP events on the library's stream, {steps} passes "
-                                                            f"after {warmup} warm-up passes",
+                                                            f"after {warmup} warm-up and {steps} timed passes",
               "mfma": {"achieved": 2048.0 * nq * n / (kms * 1e-3) / 1e12, "peak": MFMA_FP4_PEAK_TOPS, "unit": "TOPS",
                        "frac": 2048.0 * nq * n / (kms * 1e-3) / 1e12 / MFMA_FP4_PEAK_TOPS}}
         tag = f"c3_n{n}_nq{nq}_g1"
