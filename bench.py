@@ -706,10 +706,18 @@ def run_c5(a, world, rank, dev):
         out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
                                               a.k, m, threads=cpu_threads(a))
         out["cpu_gpu_identity"] = c5_identity(codes, x8, qf, P.final, a.k, cpu_threads(a))
-    print(json.dumps(out), flush=True)
+    emit(out)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def emit(rec):
+    """Rank 0's one JSON line (a VRQ_BENCH_SHARED_GPU rehearsal says so in the line)."""
+    if os.environ.get("VRQ_BENCH_SHARED_GPU") == "1":
+        rec["rehearsal"] = (f"{rec.get('n_gpus')} ranks sharing cuda:0 over gloo: exercises the N > 1 code path, "
+                            "not a measurement")
+    print(json.dumps(rec), flush=True)
 
 
 def visible_gpus(env=None, topology="/sys/class/kfd/kfd/topology/nodes") -> int:
@@ -806,7 +814,10 @@ def spawn_ranks(n: int, build: bool = True) -> int:
 def main():
     a = parse()
     # --launch-probe (CPU tests of the launcher): pretend N devices, rendezvous over gloo, no GPU work
-    plan = launch_plan(a.gpus, os.environ, a.gpus if a.launch_probe else visible_gpus())
+    # VRQ_BENCH_SHARED_GPU=1 (rehearsal of the N > 1 path on a one-GPU box): every rank runs on cuda:0 and
+    # the group is gloo (RCCL refuses two ranks on one device); the line is marked and is no measurement
+    shared = os.environ.get("VRQ_BENCH_SHARED_GPU") == "1"
+    plan = launch_plan(a.gpus, os.environ, a.gpus if (a.launch_probe or shared) else visible_gpus())
     if plan[0] == "refuse":
         log(f"bench.py: {plan[1]}")
         sys.exit(2)
@@ -825,11 +836,16 @@ def main():
         if rank == 0:
             print(json.dumps(rec), flush=True)
         return
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if a.config == "c5":
         return run_c5(a, world, rank, dev)
     if a.config == "c3":
@@ -952,7 +968,7 @@ def run_c3(a, world, rank, dev):
     if "cpu_baseline" in leg:
         out["cpu_baseline"] = leg["cpu_baseline"]
         out["cpu_gpu_identity"] = leg["cpu_gpu_identity"][str(nq)]
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
 def cpu_shard_candidates(lib, codes_h, x8_of, row0, qf_h, qb_h, K, threads):
@@ -1196,7 +1212,7 @@ def run_3phase(a, world, rank, dev):
         out["roofline_phase1"] = phase1_leg(dev, CONFIGS["c3"]["n"], PHASE1_NQS, a.k, a.binary_oversample,
                                             a.steps, a.warmup, threads, cpu=not a.no_cpu_baseline)
         log(f"[rank 0] Phase-I leg in {time.perf_counter() - t0:.1f} s")
-    print(json.dumps(out), flush=True)
+    emit(out)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
