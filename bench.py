@@ -219,16 +219,20 @@ def recall_at_10(top_rows, qf, n_total, rank, world, dev, sample):
     C = synth.centres(1024, dev)
     cs = synth.chunk_grid(n_total)
     r0, r1 = synth.shard_range(n_total, rank, world)
-    best_v = torch.full((qs.shape[0], 10), -float("inf"), device=dev)
-    best_i = torch.full((qs.shape[0], 10), -1, dtype=torch.int64, device=dev)
-    for c in range(r0 // cs, (r1 + cs - 1) // cs):
-        a, b = c * cs, min((c + 1) * cs, n_total)
-        F = synth.float_rows(a, b - a, 1024, dev, C, chunk=c)
-        S = qs @ F.T
-        v, i = torch.topk(torch.cat([best_v, S], 1), 10, dim=1)
-        cand = torch.cat([best_i, torch.arange(a, b, device=dev).expand(qs.shape[0], -1)], 1)
-        best_v, best_i = v, torch.gather(cand, 1, i)
-        del F, S
+
+    def local():
+        best_v = torch.full((qs.shape[0], 10), -float("inf"), device=dev)
+        best_i = torch.full((qs.shape[0], 10), -1, dtype=torch.int64, device=dev)
+        for c in range(r0 // cs, (r1 + cs - 1) // cs):
+            a, b = c * cs, min((c + 1) * cs, n_total)
+            F = synth.float_rows(a, b - a, 1024, dev, C, chunk=c)
+            S = qs @ F.T
+            v, i = torch.topk(torch.cat([best_v, S], 1), 10, dim=1)
+            cand = torch.cat([best_i, torch.arange(a, b, device=dev).expand(qs.shape[0], -1)], 1)
+            best_v, best_i = v, torch.gather(cand, 1, i)
+            del F, S
+        return best_v, best_i
+    best_v, best_i = in_turns(local, rank, world)
     if world > 1:
         gv = [torch.empty_like(best_v) for _ in range(world)]
         gi = [torch.empty_like(best_i) for _ in range(world)]
@@ -654,9 +658,8 @@ def run_c5(a, world, rank, dev):
     n = a.n or CONFIGS["c5"]["n"]
     nq = a.nq or CONFIGS["c5"]["nq"]
     t_setup = time.perf_counter()
-    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+    shard, qf, qb = make_data(n, nq, rank, world, dev)
     codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
-    qf, qb, _ = synth.make_queries(n, nq, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] c5 data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
     P = C5Pipeline(codes, x8, norms, row0, qf, a.k, world)
@@ -710,6 +713,33 @@ def run_c5(a, world, rank, dev):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def make_data(n, nq, rank, world, dev):
+    """This rank's rows of the synthetic corpus and the query batch (the same on every rank).  In a
+    VRQ_BENCH_SHARED_GPU rehearsal the ranks take turns (their generation transients would not fit one
+    GPU together) and return the cached blocks."""
+    def gen():
+        shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+        qf, qb, _ = synth.make_queries(n, nq, device=dev)
+        return shard, qf, qb
+    return in_turns(gen, rank, world)
+
+
+def in_turns(fn, rank, world):
+    """fn() (no collective inside); in a VRQ_BENCH_SHARED_GPU rehearsal the ranks run it one after
+    another and release their allocator caches in between, so that the transients of N ranks never
+    meet on the one GPU."""
+    if os.environ.get("VRQ_BENCH_SHARED_GPU") != "1" or world == 1:
+        return fn()
+    out = None
+    for r in range(world):
+        if r == rank:
+            out = fn()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        dist.barrier()
+    return out
 
 
 def emit(rec):
@@ -1086,9 +1116,8 @@ def run_3phase(a, world, rank, dev):
     nq = a.nq or cfg["nq"]
     N.load()
     t_setup = time.perf_counter()
-    shard = synth.make_corpus(n, rank=rank, world=world, device=dev)
+    shard, qf, qb = make_data(n, nq, rank, world, dev)
     codes, x8, norms, row0 = shard["codes"], shard["x8"], shard["norms"], shard["row0"]
-    qf, qb, _ = synth.make_queries(n, nq, device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] data ready in {time.perf_counter() - t_setup:.1f} s: shard rows {codes.shape[0]}")
 
