@@ -593,11 +593,14 @@ def cpu_baseline_c5(codes_h, x8_h, qf_h, k, n, nq_s=4, threads=16):
                       f"2*unpackbits-1; float32 dot / float64 norm), {t:.1f} s, scaled by n/{rs}"}
 
 
-def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517)):
+def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517), row0=0, world=1, rank=0):
     """Config-5 identity on the host: the oracle's reference scores (oracle_np.exhaustive_scores:
     CohereEnhancedVectorDB.py:283-293 / :302-318) of EVERY row for a few queries of the batch, their
     (score desc, row asc) top-k, against the GPU's rows and scores -- both phases.  Row blocks run
-    on ``threads`` host threads (NumPy releases the GIL inside its kernels)."""
+    on ``threads`` host threads (NumPy releases the GIL inside its kernels).  With N > 1 ranks each
+    rank scores its own shard (global rows row0 + i) and keeps its top-k; rank 0 merges the shards'
+    lists by (score desc, row asc) -- the union holds the global top-k -- and compares the merged GPU
+    result (`out`); collective over the default group, None on the other ranks."""
     import concurrent.futures as cf
     from oracle import oracle_np as O
     t0 = time.perf_counter()
@@ -605,7 +608,7 @@ def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517)):
     codes_h, x8_h, q_h = codes.cpu().numpy(), x8.cpu().numpy(), qf[qs].cpu().numpy()
     n = codes_h.shape[0]
     blk = 1 << 18
-    res = {}
+    part_top = {}
     with cf.ThreadPoolExecutor(max_workers=threads) as ex:
         for mode in ("binary", "int8_cosine"):
             S = np.empty((len(qs), n), np.float64)
@@ -615,14 +618,47 @@ def c5_identity(codes, x8, qf, out, k, threads, qsel=(5, 517)):
                 S[:, a:b] = O.exhaustive_scores(mode, q_h, codes=codes_h[a:b], x8=x8_h[a:b])
             list(ex.map(part, range(0, n, blk)))
             ref = O.exhaustive_topk(S, k)
-            m = {"binary": 2, "int8_cosine": 3}[mode]
-            g_rows = out[m][1][qs].cpu().numpy()
-            g_sc = out[m][2][qs].cpu().numpy()
-            res[mode] = {"rows_identical": bool(np.array_equal(g_rows, ref)),
-                         "scores_identical": bool(np.array_equal(g_sc, np.take_along_axis(S, ref, 1)))}
+            part_top[mode] = (ref + row0, np.take_along_axis(S, ref, 1))
+    part_top["rows"] = n
     del codes_h, x8_h
-    return {"queries": qs, "rows": n, "k": k, "seconds": time.perf_counter() - t0, **res,
-            "checker": "oracle_np.exhaustive_scores over every row on the host (test infrastructure)"}
+    parts = [part_top]
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, part_top)
+    if rank != 0:
+        return None
+    res = {}
+    for mode in ("binary", "int8_cosine"):
+        m = {"binary": 2, "int8_cosine": 3}[mode]
+        rows = np.concatenate([p[mode][0] for p in parts], 1)
+        sc = np.concatenate([p[mode][1] for p in parts], 1)
+        ref_rows = np.empty((len(qs), k), np.int64)
+        ref_sc = np.empty((len(qs), k), np.float64)
+        for i in range(len(qs)):
+            o = np.lexsort((rows[i], -sc[i]))[:k]
+            ref_rows[i], ref_sc[i] = rows[i][o], sc[i][o]
+        g_rows = out[m][1][qs].cpu().numpy()
+        g_sc = out[m][2][qs].cpu().numpy()
+        res[mode] = {"rows_identical": bool(np.array_equal(g_rows, ref_rows)),
+                     "scores_identical": bool(np.array_equal(g_sc, ref_sc))}
+    return {"queries": qs, "rows": sum(p["rows"] for p in parts), "k": k, "seconds": time.perf_counter() - t0,
+            **res, "checker": "oracle_np.exhaustive_scores over every row on the host (test infrastructure)"
+            + ("; each rank its shard, merged on rank 0 by (score desc, row asc)" if world > 1 else "")}
+
+
+def c5_multi_gpu_fields(st, dev):
+    """Config 5's N > 1 fields: process group, per-rank spread of the two main passes, the exchange time
+    (the two gather_topk + merge_topk_shards).  Collective over the default group."""
+    world = dist.get_world_size()
+    mine = torch.tensor([st["binary_main"], st["cosine_main"], st["collective"]], dtype=torch.float64, device=dev)
+    allr = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    allr = torch.stack(allr).cpu().numpy()
+    return {"world_size_process_group": world, "backend": dist.get_backend(),
+            "rank_binary_main_ms": {"min": float(allr[:, 0].min()), "max": float(allr[:, 0].max())},
+            "rank_cosine_main_ms": {"min": float(allr[:, 1].min()), "max": float(allr[:, 1].max())},
+            "gather_merge_ms_max_over_ranks": float(allr[:, 2].max()),
+            "collective": "per phase one all_gather of the per-shard top-k (rows, scores) + merge_topk_shards"}
 
 
 def timed_loop(P, a, world, dev):
@@ -667,12 +703,18 @@ def run_c5(a, world, rank, dev):
     rec = None
     if not a.no_recall:
         rec = recall_at_10(P.final[3][1], qf, n, rank, world, dev, min(a.recall_sample, nq))
+    st = P.stage_ms()
+    multi = None
+    if world > 1:
+        multi = c5_multi_gpu_fields(st, dev)
+        if not a.no_cpu_baseline:
+            multi["sample_check"] = c5_identity(codes, x8, qf, P.final, a.k, cpu_threads(a), row0=row0,
+                                                world=world, rank=rank)
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
-    st = P.stage_ms()
     m = codes.shape[0]
     ops = 2.0 * nq * m * 1024  # algorithmic MACs x 2 per phase
     tag = f"c5_n{n}_nq{nq}_g{world}"
@@ -704,6 +746,8 @@ def run_c5(a, world, rank, dev):
                    "parallelism": f"row-shard x{world} + RCCL all_gather" if world > 1 else "1 GPU"},
         "recall_at_10": rec, "phase_ms": st, "roofline": roof, "roofline_binary": roof_bin,
     }
+    if multi is not None:
+        out["multi_gpu"] = multi
     if world == 1 and not a.no_cpu_baseline:
         rs = min(m, 1_000_000)
         out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
