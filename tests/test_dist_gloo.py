@@ -190,3 +190,58 @@ def test_two_rank_gloo_config5_topk_merge_equals_single_corpus():
         p.join(240)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+def _worker_c5_identity(rank, world, port, result_q):
+    """bench.py's config-5 N > 1 identity check (c5_identity with row0/world/rank): each rank scores its
+    shard with the oracle, rank 0 merges by (score desc, row asc) and compares `out` -- here the
+    oracle's whole-corpus top-k (must be identical) and a copy with two ranks of one list swapped
+    (must not)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    rng = np.random.default_rng(5)
+    n, nq, k = 3000, 8, 10
+    codes = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    x8 = rng.integers(-127, 128, (n, 1024), dtype=np.int8)
+    codes[1600:1700], x8[1600:1700] = codes[0:100], x8[0:100]  # exact ties across the shard boundary
+    qf = (rng.standard_normal((nq, 1024)) * 0.03).astype(np.float32)
+    qsel = (1, 5)
+    out = {}
+    for mode, m in (("binary", 2), ("int8_cosine", 3)):
+        S = O.exhaustive_scores(mode, qf, codes=codes, x8=x8)
+        top = O.exhaustive_topk(S, k)
+        out[m] = (torch.full((nq,), k, dtype=torch.int32), torch.from_numpy(top.astype(np.int64)),
+                  torch.from_numpy(np.take_along_axis(S, top, 1)))
+    r0, r1 = synth.shard_range(n, rank, world)
+    args = (torch.from_numpy(codes[r0:r1]), torch.from_numpy(x8[r0:r1]), torch.from_numpy(qf))
+    good = bench.c5_identity(*args, out, k, 2, qsel=qsel, row0=r0, world=world, rank=rank)
+    bad_out = {m: (c, r.clone(), s) for m, (c, r, s) in out.items()}
+    for m in (2, 3):
+        bad_out[m][1][5, [0, 1]] = bad_out[m][1][5, [1, 0]]
+    bad = bench.c5_identity(*args, bad_out, k, 2, qsel=qsel, row0=r0, world=world, rank=rank)
+    if rank == 0:
+        ok = all(good[mo]["rows_identical"] and good[mo]["scores_identical"] for mo in ("binary", "int8_cosine"))
+        ok = ok and good["rows"] == n
+        ok = ok and not any(bad[mo]["rows_identical"] for mo in ("binary", "int8_cosine"))
+        result_q.put(bool(ok))
+    else:
+        result_q.put(good is None and bad is None)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_bench_config5_identity_check():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c5_identity, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True and q.get(timeout=5) is True
