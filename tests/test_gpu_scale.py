@@ -5,7 +5,9 @@
   bit, the VRQ_SEARCH_SHARD searches of the 8 row ranges an 8-GPU run would own, merged by
   vrq_merge_shards (the multi-GPU semantics of CohereEnhancedVectorDB.py:267-322); the single index's
   Phase I equals the FAISS hammings_knn_hc restatement and its final rows and Phase-II scores equal the
-  reference NumPy Phases II/III on 16 queries spread over both 512-query blocks.
+  reference NumPy Phases II/III on 16 queries spread over both 512-query blocks (rows and Phase-II
+  scores bit for bit, Phase-III cosines within 1e-5 relative).
+* The same equality for 8 row ranges of 500K rows, each short enough (n * nq <= 2^32) to run K1s.
 * ShardedSearch through a real ``nccl`` (RCCL) process group.
 * ``CohereEnhancedVectorDB`` / ``CohereVectorDBFloat`` opening byte copies of the reference's persisted
   folders (tests/golden/ref_db: FAISS index + RocksDB tables) and reproducing its search output.
@@ -42,7 +44,8 @@ def _phase23_reference(qf, codes_rows, x8_rows, rows, k=10, osi=3):
         nrm = np.linalg.norm(x8_rows[j])
         s3.append(-np.inf if nrm == 0 else float(qf.dot(x8_rows[j])) / nrm)
     o3 = sorted(range(len(o2)), key=lambda j: -s3[j])[:k]
-    return np.array([rows[o2[j]] for j in o3], dtype=np.int64), np.array([s2[o2[j]] for j in o3])
+    return (np.array([rows[o2[j]] for j in o3], dtype=np.int64), np.array([s2[o2[j]] for j in o3]),
+            np.array([s3[j] for j in o3]))
 
 
 def test_100m_row_ranges_merge_equal_single_index(dev, oracle_lib):
@@ -80,10 +83,47 @@ def test_100m_row_ranges_merge_equal_single_index(dev, oracle_lib):
     for i, q in enumerate(qsel):
         rows = I[i]
         x8r = x8[torch.from_numpy(rows).to(dev)].cpu().numpy()
-        ref_rows, ref_s2 = _phase23_reference(qf_h[q], codes_h[rows], x8r, rows)
+        ref_rows, ref_s2, ref_s3 = _phase23_reference(qf_h[q], codes_h[rows], x8r, rows)
         assert np.array_equal(full[1][q], ref_rows)
         assert np.array_equal(full[3][q], ref_s2)
+        # Phase III: exact f64 dot rounded once vs NumPy's f32 sdot, within 1e-5 relative
+        np.testing.assert_allclose(full[4][q], ref_s3, rtol=1e-5, atol=1e-7)
     del codes_h, sh, codes, x8, norms
+    torch.cuda.empty_cache()
+
+
+def test_k1s_row_ranges_merge_equal_single_index(dev, oracle_lib):
+    """8 row ranges of 500K rows at nq = 1024 (per-shard n * nq <= 2^32: every shard runs K1s, as
+    config 2 does at N = 8), merged by vrq_merge_shards, equal the single 4M-row index bit for bit."""
+    from vectorragquantization_amd import _native as N
+    from vectorragquantization_amd import synth
+    from vectorragquantization_amd.dist import merge_shards
+    from vectorragquantization_amd.enhanced import search3
+
+    n, nq, k = 4_000_000, 1024, 10
+    sh = synth.make_corpus(n, device=dev)
+    codes, x8, norms = sh["codes"], sh["x8"], sh["norms"]
+    qf, qb, _ = synth.make_queries(n, nq, device=dev)
+    full = [t.cpu().numpy() for t in search3(codes, x8, norms, qf, qb, k, 100, 30)]
+    info = np.zeros(12, np.int64)
+    parts = []
+    for g in range(8):
+        r0, r1 = synth.shard_range(n, g, 8)
+        N.check(N.load().vrq_scan_plan(r1 - r0, 1024, nq, 100, 0, info.ctypes.data), "plan")
+        assert int(info[0]) == 2, "shard does not run K1s"
+        parts.append(search3(codes[r0:r1], x8[r0:r1], norms[r0:r1], qf, qb, k, 100, 30, N.VRQ_SEARCH_SHARD, r0))
+    st = [torch.stack([p[i] for p in parts]) for i in range(5)]
+    merged = [t.cpu().numpy() for t in merge_shards(st[0], st[1], st[2], st[3], st[4], k, 30)[:5]]
+    for a, b in zip(merged, full):
+        assert np.array_equal(a, b), "8 merged K1s row ranges differ from the single index"
+    assert (full[0] == k).all()
+    # the single index's Phase I (K1s at 4M x 1024) vs the FAISS restatement on a query sample
+    qsel = np.linspace(0, nq - 1, 32).round().astype(np.int64)
+    p1 = [t.cpu().numpy() for t in search3(codes, x8, norms, qf, qb, k, 100, 30, N.VRQ_SEARCH_PHASE1_ONLY)]
+    D, I = oracle_knn(oracle_lib, codes.cpu().numpy(), qb[torch.from_numpy(qsel).to(dev)].cpu().numpy(), 100,
+                      threads=16)
+    assert np.array_equal(p1[2][qsel], D) and np.array_equal(p1[1][qsel], I)
+    del sh, codes, x8, norms
     torch.cuda.empty_cache()
 
 

@@ -36,6 +36,20 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the vrq HIP library cannot be built")
 
 
+_TOOLCHAIN = None
+
+
+def _toolchain_id() -> str:
+    """`hipcc --version` plus the compile-flag environment hipcc reads: part of each object's stamp."""
+    global _TOOLCHAIN
+    if _TOOLCHAIN is None:
+        r = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True)
+        env = [f"{k}={os.environ[k]}" for k in ("HIPCC_COMPILE_FLAGS_APPEND", "HIPCC_LINK_FLAGS_APPEND",
+                                               "HIP_CLANG_PATH", "ROCM_PATH") if k in os.environ]
+        _TOOLCHAIN = "\n".join([r.stdout.strip(), *env])
+    return _TOOLCHAIN
+
+
 def _deps() -> list:
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
         os.path.join(os.path.dirname(PKG), "include", "vrq.h")]
@@ -77,20 +91,25 @@ def _build_one(lib: str, probe: bool, verbose: bool, force_all: bool = False) ->
         cmd = [hipcc, *CFLAGS, *(["-DVRQ_TUNING_ENV"] if probe else []), *EXTRA.get(src, []), "-c",
                os.path.join(CSRC, src), "-o", obj]
         # incremental: an object newer than its source and every header, built by the same command
+        # (the stamp names the toolchain and the flag environment too, and is removed before hipcc runs,
+        # so an interrupted compile or a toolchain change never leaves a stale object looking current)
         stamp = obj + ".cmd"
+        stamp_text = "\n".join([" ".join(cmd), _toolchain_id()])
         if not force_all and os.path.exists(obj) and os.path.exists(stamp):
             t = os.path.getmtime(obj)
             with open(stamp) as f:
-                same = f.read() == " ".join(cmd)
+                same = f.read() == stamp_text
             if same and all(os.path.getmtime(d) <= t for d in [os.path.join(CSRC, src), *headers]):
                 return obj
+        if os.path.exists(stamp):
+            os.remove(stamp)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
         if verbose and r.stderr:
             print(r.stderr, file=sys.stderr)
         with open(stamp, "w") as f:
-            f.write(" ".join(cmd))
+            f.write(stamp_text)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=8) as ex:

@@ -133,7 +133,8 @@ class BinaryIndexIDMap2:
 
     def add_with_ids(self, x, ids) -> None:
         x = as_device_tensor(x, torch.uint8, self.device).reshape(-1, self.code_size)
-        ids_np = np.asarray(ids.cpu() if isinstance(ids, torch.Tensor) else ids, dtype=np.int64).reshape(-1)
+        # a private, writable copy (torch.from_numpy warns on read-only arrays, e.g. a mmap'd index.bin)
+        ids_np = np.array(ids.cpu() if isinstance(ids, torch.Tensor) else ids, dtype=np.int64, copy=True).reshape(-1)
         if ids_np.shape[0] != x.shape[0]:
             raise ValueError("add_with_ids: codes and ids differ in length")
         base = self.ntotal
