@@ -753,11 +753,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 // 64 AGPRs, unpacked once per row set) and streams the workgroup's 512 queries from LDS as packed bits
 // (64 KiB, loaded once per workgroup), unpacking each query k-step with 5 VALU ops:
 //   * per 32-query block: 16 k-steps x SRB MFMAs (32x32x64 FP4), each B fragment (one dword per lane)
-//     feeding SRB MFMAs; 4 ds_read_b128 of queries per block and wave (64 B of LDS reads per MFMA, a
-//     quarter of K1m's); no LDS writes and no barrier inside the loop;
-//   * each wave owns every 4th row set of the workgroup's chunk and LDS-DMAs the next one into its own
-//     16 KiB staging buffer a whole row set (~16 query blocks) ahead; at the row-set switch it
-//     rebuilds its A fragments and row popcounts from there;
+//     feeding SRB MFMAs; 4 ds_read_b128 of queries per block and wave; no LDS writes and no barrier
+//     inside the loop;
+//   * each of the SNW waves owns every SNW-th row set of the workgroup's chunk and LDS-DMAs the next one
+//     into its own staging buffer (SRB x 4 KiB) a whole row set (16 query blocks) ahead;
 //   * lane (j, h) of a 32x32 accumulator holds query j of the block and rows (g&3) + 8(g>>2) + 4h of
 //     the row block.  Seeds 1024 - pc(r)/2 (per register, from LDS) make acc = 1024 + <q,r> - pc(r)/2,
 //     always > 0 for a row of the chunk (-4096 seeds mask the rows past its end), so the candidate
@@ -765,8 +764,18 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 //     bit patterns and one compare per lane against its query's threshold (thr > 0: tau <= 1025);
 //     v = dist - tau(q) = 2 thr - 2 acc exactly;
 //   * the test of a block's accumulators runs in the next block's MFMA shadow (two accumulator sets);
-//     hits are staged per wave and appended to the per-(query, chunk) lists once per row set, at
-//     positions taken from the workgroup's per-query LDS counters (the four waves share the chunk).
+//     hits are staged per wave and appended to the per-(query, chunk) lists at positions taken from the
+//     workgroup's per-query LDS counters (the waves share the chunk).  The stage is flushed at the first
+//     block of each row set and whenever it holds more than STG/2 entries after a block's test, so an
+//     overflow can only come from the one block just tested: it marks that block's 32 queries'
+//     lists overflowed (exact rescan), not the workgroup's 512.
+// Two instances:
+//   * <SRB = 2, SNW = 8>: two waves per SIMD (256 registers each; 64-row sets); at the row-set switch a
+//     wave rebuilds its A fragments and seeds from the staging buffer while the SIMD's other wave runs.
+//   * <SRB = 4, SNW = 4>: one wave per SIMD (A = all 256 AGPRs; 128-row sets): each query fragment feeds
+//     4 MFMAs (half the unpack VALU and query reads per MFMA) and the row-set switch is spread over the
+//     last query block of the set -- k-step s's new A fragments are unpacked right after that k-step's
+//     MFMAs, from staging reads issued one block ahead -- so the matrix core does not wait for it.
 // The lists, their keys and the suffix merge are K1m's, so the pass is a drop-in for K1m's MB = 4
 // instance (same launch geometry: one workgroup per (chunk, 512-query block)).
 // K1s takes the large-batch pass up to this many (query, row) pairs per launch (1M rows x 1024 queries:
@@ -775,21 +784,30 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 // pass is power-bound -- 100M x 1024 in the config-4 bench ran 32.8 ms on K1s vs 31.0 on K1m on one box
 // (K1s 2.22 GHz / 0.75 of the matrix cores busy vs K1m 2.37 GHz / 0.71; profiles/r5_k1s_ab.jsonl).
 constexpr double kSwapMaxPairs = 4294967296.0;
-constexpr int SRB = 2;          // row blocks of 32 rows per row set
-constexpr int SNW = 8;          // waves per workgroup (two per SIMD)
-constexpr int SRS = SRB * 32;   // rows per row set (128)
-constexpr int SQPB = 512;       // queries per workgroup (16 blocks of 32)
+// A/B builds only (tools/build_variants.sh -D...): VRQ_K1S_LARGE=1 runs passes above kSwapMaxPairs on
+// K1s<4, 4> instead of K1m; VRQ_K1S_RB4=1 runs the shorter ones on K1s<4, 4> instead of K1s<2, 8>
+#ifndef VRQ_K1S_LARGE
+#define VRQ_K1S_LARGE 0
+#endif
+#ifndef VRQ_K1S_RB4
+#define VRQ_K1S_RB4 0
+#endif
+constexpr int SQPB = 512;  // queries per workgroup (16 blocks of 32)
+template <int SRB, int SNW>
 struct SwapShape {
-  static constexpr int QBYTES = SQPB * 128;          // packed queries (swizzled 16-B pieces)
-  static constexpr int RBYTES = SRS * 128;           // one wave's row staging
+  static constexpr int SRS = SRB * 32;      // rows per row set
+  static constexpr int QBYTES = SQPB * 128;  // packed queries (swizzled 16-B pieces)
+  static constexpr int RBYTES = SRS * 128;   // one wave's row staging
   static constexpr int SMEM = QBYTES + SNW * RBYTES + SQPB * 4 /* thr */ + SQPB * 4 /* list lengths */ +
                               SNW * (STG + 1) * 4 + SNW * SRB * 32 * 4 /* seeds */;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(SRS <= 128, "a staged entry keeps 7 bits of row in the row set");
+  static_assert((SRB == 2 && SNW == 8) || (SRB == 4 && SNW == 4), "the two instances");
 };
 // staged hit entry of K1s (u32): (v + 1025) << 16 | query-in-workgroup << 7 | row in the row set
 constexpr int SENT_V_SHIFT = 16, SENT_Q_SHIFT = 7;
 
-template <int MODE>
+template <int MODE, int SRB, int SNW>
 __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     const uint8_t* __restrict__ codes, int64_t n, int64_t row_begin, const uint8_t* __restrict__ queries, int nq,
     const int32_t* __restrict__ tau, uint64_t* __restrict__ cand, int32_t* __restrict__ ccnt, int capc,
@@ -797,11 +815,17 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     const int32_t* __restrict__ rerun, const int32_t* __restrict__ qbflag, uint16_t* __restrict__ dv,
     int64_t dv_stride) {
   static_assert(MODE == MFMA_MAIN || MODE == MFMA_RERUN, "thresholded passes only");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[SwapShape::SMEM];
+  using Sh = SwapShape<SRB, SNW>;
+  constexpr int SRS = Sh::SRS;
+#ifndef VRQ_K1S_SPREAD
+#define VRQ_K1S_SPREAD 1
+#endif
+  constexpr bool SPREAD = SNW == 4 && VRQ_K1S_SPREAD;  // one wave per SIMD: the switch is spread over a block
+  __shared__ __attribute__((aligned(16))) uint8_t smem[Sh::SMEM];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* qpk = smem;
-  uint8_t* rst = smem + SwapShape::QBYTES + w * SwapShape::RBYTES;  // this wave's row staging
-  float* thr = reinterpret_cast<float*>(smem + SwapShape::QBYTES + SNW * SwapShape::RBYTES);
+  uint8_t* rst = smem + Sh::QBYTES + w * Sh::RBYTES;  // this wave's row staging
+  float* thr = reinterpret_cast<float*>(smem + Sh::QBYTES + SNW * Sh::RBYTES);
   int32_t* lcnt = reinterpret_cast<int32_t*>(thr + SQPB);
   int32_t* stg = lcnt + SQPB + w * (STG + 1);
   float* sdw = reinterpret_cast<float*>(lcnt + SQPB + SNW * (STG + 1)) + w * SRB * 32;
@@ -817,7 +841,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const int64_t row0 = row_begin + (int64_t)chunk * chunk_stride;
   const int64_t row1 = (row0 + chunk_rows < n) ? row0 + chunk_rows : n;
   if (row0 >= row1) return;
-  const int nrs = (int)((row1 - row0 + SRS - 1) / SRS);  // row sets of the chunk; wave w takes w, w + 4, ...
+  const int nrs = (int)((row1 - row0 + SRS - 1) / SRS);  // row sets of the chunk; wave w takes w, w + SNW, ...
   const int qbase = qb * SQPB;
   const int nqv = nq - qbase < SQPB ? nq - qbase : SQPB;
   const int nqblk = (((nqv + 31) >> 5) + 1) & ~1;  // query blocks, run in pairs
@@ -884,9 +908,11 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const int64_t qstride = (int64_t)nchunks * capc;
   uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;  // + ql * qstride + pos
   int nst = 0;  // staged entries (wave-uniform)
-  auto flush = [&](int64_t base_row) __attribute__((always_inline)) {  // staged hits -> lists
-    if (nst > STG) {  // the stage overflowed: every list of the workgroup -> exact rescan
-      for (int i = l; i < SQPB; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
+  // staged hits -> lists; all staged entries are of rows of one row set (first row base_row), and any
+  // entry past STG was a hit of query block qblk (the one block tested since the stage last held <= STG/2)
+  auto flush = [&](int64_t base_row, int qblk) __attribute__((always_inline)) {
+    if (nst > STG) {  // the stage overflowed: that block's 32 queries' lists -> exact rescan
+      if (l < 32) lds_add32(lc0 + (uint32_t)((qblk * 32 + l) * 4), capc + 1);
       nst = STG;
     }
     for (int i0 = 0; i0 < nst; i0 += 64) {
@@ -947,6 +973,13 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const int nmine = w < nrs ? (nrs - w + SNW - 1) / SNW : 0;  // this wave's row sets
   if (nmine > 0) {
     v4i A[SRB][KS];  // [rb][s]: dword 16h + s of row 32rb + ri of the row set, as 32 e2m1 values
+    // seed of block row ri of row block rb at sdw[rb][hh][g], ri = (g & 3) + 8 (g >> 2) + 4 hh (lane halves
+    // read 16 floats each); pc = the row's popcount, r = its row in the set
+    auto write_seed = [&](int rb, int pc, int64_t r0) __attribute__((always_inline)) {
+      const float sv = r0 + 32 * rb + ri < row1 ? 1024.0f - 0.5f * (float)pc : -4096.0f;
+      if (h == 0)
+        lds_write32(sdw0 + (uint32_t)((rb * 32 + ((ri >> 2) & 1) * 16 + (ri & 3) + 4 * (ri >> 3)) * 4), __float_as_int(sv));
+    };
     // the row set's A fragments and seeds from the staging buffer (its DMA landed)
     auto rebuild = [&](int64_t r0) __attribute__((always_inline)) {
       static_for<0, SRB>([&](auto RB) {
@@ -965,10 +998,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
           asm volatile("" : "+a"(A[rb][s]));  // straight to the accumulator file
         }
         pc += __shfl_xor(pc, 32, 64);  // both halves of the row
-        // seed of block row ri at [rb][hh][g], ri = (g & 3) + 8 (g >> 2) + 4 hh: lane halves read 16 floats each
-        const float sv = r0 + r < row1 ? 1024.0f - 0.5f * (float)pc : -4096.0f;
-        if (h == 0)
-          lds_write32(sdw0 + (uint32_t)((rb * 32 + ((ri >> 2) & 1) * 16 + (ri & 3) + 4 * (ri >> 3)) * 4), __float_as_int(sv));
+        write_seed(rb, pc, r0);
       });
     };
     // this lane half's 16 seeds of row block rb, as four 16-B reads
@@ -982,6 +1012,17 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
                                              4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
       return __builtin_bit_cast(v16f, x);
     };
+    // the same, retired at once (the end of a spread switch: no copy of a register before its read lands)
+    auto read_seed_now = [&](int rb) __attribute__((always_inline)) {
+      v4i p[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lds_read128(p[i], sdw0 + (uint32_t)(rb * 128 + h * 64 + i * 16));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3])::"memory");
+      const v16i x = __builtin_shufflevector(__builtin_shufflevector(p[0], p[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                             __builtin_shufflevector(p[2], p[3], 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3,
+                                             4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      return __builtin_bit_cast(v16f, x);
+    };
     // query block qbi's B dwords (k-steps 4i..4i+3 in wq[i]) and this lane's threshold
     auto read_qblock = [&](v4i (&wq)[4], int& thb, int qbi) __attribute__((always_inline)) {
       const int j = qbi * 32 + ri;
@@ -990,37 +1031,84 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
       lds_read32_inplace(thb, thr0 + (uint32_t)(j * 4));
     };
 
-    wait_vm<0>();
-    rebuild(row0 + (int64_t)w * SRS);
-    if (nmine > 1) issue(w + SNW);
     v16f acc[2][SRB];
     v4i wq[2][4] = {};
     int thb[2] = {};
-    static_for<0, SRB>([&](auto RB) { acc[0][RB] = read_seed(RB); });
-    read_qblock(wq[0], thb[0], 0);
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                   "+v"(wq[0][3]), "+v"(thb[0])::"memory");
-
-    bool have_prev = false;      // an untested block in acc[1 - parity]
-    int prev_qb = 0;             // its query block
-    int64_t set_base = row0 + (int64_t)w * SRS;  // first row of the current row set
-    int64_t prev_base = set_base;                 // ... of the row set the staged hits belong to
-    // one query block: k-step s runs SRB MFMAs on the unpacked dword s of wq[c]; in the shadow: the
-    // previous block's test (s = 1), the previous row set's flush (s = 2, first block of a set), the
-    // next block's seeds, B dwords and threshold (s = 3), retired at the top of the next block
-    auto qblock = [&](auto PAR, int qbi, bool last) __attribute__((always_inline)) {
-      constexpr int c = decltype(PAR)::value;
-      {  // retire the reads of the previous block (this block's operands; a no-op before the first)
-        static_assert(SRB == 2, "the wait names the two row blocks' accumulators");
+    // retire every LDS read, naming the registers of parity c (accumulator seeds, B dwords, threshold)
+    auto retire = [&](auto C) __attribute__((always_inline)) {
+      constexpr int c = decltype(C)::value;
+      (void)acc, (void)wq, (void)thb;  // (odr-use outside the if constexpr: clang's implicit capture)
+      if constexpr (SRB == 2)
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(acc[c][0]), "+v"(acc[c][1]), "+v"(wq[c][0]), "+v"(wq[c][1]), "+v"(wq[c][2]),
                        "+v"(wq[c][3]), "+v"(thb[c])::"memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(acc[c][0]), "+v"(acc[c][1]), "+v"(acc[c][2]), "+v"(acc[c][3]), "+v"(wq[c][0]),
+                       "+v"(wq[c][1]), "+v"(wq[c][2]), "+v"(wq[c][3]), "+v"(thb[c])::"memory");
+    };
+    // spread switch (SPREAD): packed dwords 4i..4i+3 of the lane's half row of row block rb of the next row
+    // set (k-step group i) land in sg[rb], read in place one k-step before their group starts
+    auto stage_read = [&](v4i (&sg)[SRB], int grp) __attribute__((always_inline)) {
+      static_for<0, SRB>([&](auto RB) {
+        constexpr int rb = decltype(RB)::value;
+        lds_read128_inplace(sg[rb], rst0 + (uint32_t)(pk_slot(32 * rb + ri, 4 * h + grp) * 16));
+      });
+    };
+    auto retire_sg = [&](v4i (&sg)[SRB]) __attribute__((always_inline)) {
+      static_assert(!SPREAD || SRB == 4, "the wait names four row blocks' staging registers");
+      if constexpr (SPREAD)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sg[0]), "+v"(sg[1]), "+v"(sg[2]), "+v"(sg[3])::"memory");
+    };
+
+    wait_vm<0>();
+    rebuild(row0 + (int64_t)w * SRS);
+    if (nmine > 1) issue(w + SNW);
+    static_for<0, SRB>([&](auto RB) { acc[0][RB] = read_seed(RB); });
+    read_qblock(wq[0], thb[0], 0);
+    retire(std::integral_constant<int, 0>{});
+
+    bool have_prev = false;      // an untested block in acc[1 - parity]
+    int prev_qb = 0;             // its query block
+    int kset = 0;                // this wave's current row set (its k-th)
+    int64_t set_base = row0 + (int64_t)w * SRS;  // first row of the current row set
+    int64_t stage_base = set_base;               // ... of the row set the staged hits belong to
+    // one query block: k-step s runs SRB MFMAs on the unpacked dword s of wq[c]; in the shadow: the
+    // previous block's test (s = 1), the stage flush (s = 2), the next block's seeds, B dwords and
+    // threshold (s = 3), retired at the top of the next block.  SW (the last block of a row set with the
+    // spread switch): after k-step s's MFMAs, k-step s's A fragments of the next row set (its staging
+    // read one k-step before its group of four starts); the next set's seeds and the DMA of the set
+    // after it at the end.
+    auto qblock = [&](auto PAR, auto SWC, int qbi) __attribute__((always_inline)) {
+      constexpr int c = decltype(PAR)::value;
+      constexpr bool SW = decltype(SWC)::value;
+      retire(std::integral_constant<int, c>{});  // this block's operands (a no-op before the first)
+      v4i sg[SRB] = {};   // SW: the next row set's packed dwords of one k-step group (block-local)
+      int spc[SRB] = {};  // SW: its rows' popcounts (this lane's half row)
+      if constexpr (SW) {  // the next row set's DMA (issued a whole set ago) landed: group 0
+        wait_vm<0>();
+        stage_read(sg, 0);
       }
       static_for<0, KS>([&](auto S) {
         constexpr int s = decltype(S)::value;
         const v4i bq = unpack_row32((uint32_t)wq[c][s >> 2][s & 3]);
-        static_for<0, SRB>([&](auto RB) { acc[c][RB] = mfma_fp4(A[RB][s], bq, acc[c][RB]); });
+        static_for<0, SRB>([&](auto RB) {
+          acc[c][RB] = mfma_fp4(A[RB][s], bq, acc[c][RB]);
+          // (SW: pinned before the fence, so the MFMAs reading A[.][s] are issued before A[.][s] is replaced)
+          if constexpr (SW) asm volatile("" : "+v"(acc[c][RB]));
+        });
+        if constexpr (SW) VRQ_SCHED_FENCE();
+        if constexpr (SW) {
+          if constexpr ((s & 3) == 0) retire_sg(sg);
+          static_for<0, SRB>([&](auto RB) {
+            constexpr int rb = decltype(RB)::value;
+            const uint32_t wd = (uint32_t)sg[rb][s & 3];
+            spc[rb] += __popc(wd);
+            A[rb][s] = unpack_query32(wd);  // k-step s of this block has issued its MFMAs
+            asm volatile("" : "+a"(A[rb][s]));
+          });
+          if constexpr ((s & 3) == 3 && s < KS - 1) stage_read(sg, (s >> 2) + 1);
+        }
         if constexpr (s == 1) {
           if (have_prev) {
             const float th = __int_as_float(thb[c ^ 1]);
@@ -1041,43 +1129,63 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
           }
         }
         if constexpr (s == 2) {
-          if (qbi == 0 && have_prev) {  // every staged hit is the previous row set's
-            if (nst) flush(prev_base);
-            prev_base = set_base;
-          }
+          // the first block of a set: every staged hit is the previous row set's; otherwise flush when the
+          // stage is over half full (the entries are this set's)
+          if (have_prev && (qbi == 0 || nst > STG / 2) && nst) flush(stage_base, prev_qb);
+          if (qbi == 0) stage_base = set_base;
         }
         if constexpr (s == 3) {
           const int nxt = qbi + 1 < nqblk ? qbi + 1 : 0;
-          static_for<0, SRB>([&](auto RB) { acc[c ^ 1][RB] = read_seed(RB); });  // (re-read after a switch)
+          if constexpr (!SW) static_for<0, SRB>([&](auto RB) { acc[c ^ 1][RB] = read_seed(RB); });  // (re-read after a switch)
           read_qblock(wq[c ^ 1], thb[c ^ 1], nxt);
         }
       });
+      if constexpr (SW) {  // the next row set's seeds (its A fragments are in place), its successor's DMA
+        const int64_t nb0 = row0 + (int64_t)(w + SNW * (kset + 1)) * SRS;
+        static_for<0, SRB>([&](auto RB) {
+          constexpr int rb = decltype(RB)::value;
+          const int pc = spc[rb] + __shfl_xor(spc[rb], 32, 64);
+          write_seed(rb, pc, nb0);
+        });
+        static_for<0, SRB>([&](auto RB) { acc[c ^ 1][RB] = read_seed_now(RB); });
+        if (kset + 2 < nmine) issue(w + SNW * (kset + 2));  // (every staging read retired at k-step 12)
+        set_base = nb0;
+        ++kset;
+      }
       have_prev = true;
       prev_qb = qbi;
     };
 
+    using F = std::false_type;
+    using T = std::true_type;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    // (SPREAD: the last pair of every row set switches, the last set's too -- it then rebuilds from a
+    // stale staging buffer and nothing uses the result -- so that the loop body has one path and the
+    // A fragments one register assignment)
     for (int k = 0; k < nmine; ++k) {
-      for (int qp = 0; qp < nqblk; qp += 2) {
-        qblock(std::integral_constant<int, 0>{}, qp, false);
-        qblock(std::integral_constant<int, 1>{}, qp + 1, qp + 2 >= nqblk);
+      for (int qp = 0; qp + 2 < nqblk; qp += 2) {
+        qblock(P0{}, F{}, qp);
+        qblock(P1{}, F{}, qp + 1);
       }
-      if (k + 1 < nmine) {  // switch to the next row set: its DMA landed; start the one after
+      qblock(P0{}, F{}, nqblk - 2);
+      if constexpr (SPREAD)
+        qblock(P1{}, T{}, nqblk - 1);
+      else
+        qblock(P1{}, F{}, nqblk - 1);
+      if (!SPREAD && k + 1 < nmine) {  // switch to the next row set: its DMA landed; start the one after
         wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                       "+v"(wq[0][3]), "+v"(thb[0])::"memory");
+        retire(P0{});
         set_base = row0 + (int64_t)(w + SNW * (k + 1)) * SRS;
         rebuild(set_base);
         if (k + 2 < nmine) issue(w + SNW * (k + 2));
         static_for<0, SRB>([&](auto RB) { acc[0][RB] = read_seed(RB); });
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0][0]), "+v"(acc[0][1])::"memory");
+        retire(P0{});
       }
     }
     // the last block of the last row set
     {
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(wq[0][0]), "+v"(wq[0][1]), "+v"(wq[0][2]),
-                     "+v"(wq[0][3]), "+v"(thb[0])::"memory");
+      retire(P0{});
       const float th = __int_as_float(thb[1]);
       static_for<0, SRB>([&](auto RB) {
         const v16i x = __builtin_bit_cast(v16i, acc[1][RB]);
@@ -1086,7 +1194,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
         const int x4 = max(max(x[12], x[13]), x[14]);
         if (__ballot(max(max(max(x0, x1), x2), max(max(x3, x4), x[15])) > thb[1])) block_hits(acc[1][RB], RB, th, prev_qb);
       });
-      if (nst) flush(set_base);
+      if (nst) flush(stage_base, prev_qb);
     }
   }
   wait_lgkm0();
@@ -2031,7 +2139,11 @@ int mfma_plan(int64_t n, int nq, int K, MfmaPlan* p) {
   // large batches: K1s (row sets resident, queries streamed) for passes of <= kSwapMaxPairs (query, row)
   // pairs, K1m above (see kSwapMaxPairs)
   static_assert(SQPB == MfmaShape<kMbLarge>::QPB, "K1s serves K1m's MB = 4 query blocks");
-  p->swap = p->mb == kMbLarge && (double)n * (double)nq <= kSwapMaxPairs;
+  // (p->swap: 1 = K1s<2, 8>, 2 = K1s<4, 4>)
+  {
+    const bool short_pass = (double)n * (double)nq <= kSwapMaxPairs;
+    p->swap = p->mb != kMbLarge ? 0 : short_pass ? (VRQ_K1S_RB4 ? 2 : 1) : (VRQ_K1S_LARGE ? 2 : 0);
+  }
   // small batches (nq <= 128): the row-split kernel K1r, all queries in every wave
   // (VRQ_MFMA_ROWS=0: probe-build override)
   p->rows = nq <= kRowsMaxQueries && tuning_int("VRQ_MFMA_ROWS", 1) != 0;
@@ -2123,11 +2235,14 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
   const bool sampled = p.j < K;
   const int32_t* none = nullptr;
   // the MB = 4 or MB = 2 instance of a pass
-  auto pass = [&](auto kswap, auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd, int32_t* cc,
-                  int64_t crows, int64_t cstride, int nch, const int32_t* rr, const int32_t* qf, uint16_t* d,
-                  int64_t dstride) {
-    if (p.swap)
-      hipLaunchKernelGGL(kswap, dim3(grid), dim3(SNW * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
+  auto pass = [&](auto kswap2, auto kswap4, auto kern4, auto kern2, int grid, const int32_t* tau, uint64_t* cd,
+                  int32_t* cc, int64_t crows, int64_t cstride, int nch, const int32_t* rr, const int32_t* qf,
+                  uint16_t* d, int64_t dstride) {
+    if (p.swap == 1)
+      hipLaunchKernelGGL(kswap2, dim3(grid), dim3(8 * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
+                         crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
+    else if (p.swap == 2)
+      hipLaunchKernelGGL(kswap4, dim3(grid), dim3(4 * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
                          crows, cstride, (int64_t)RT, nch, p.nqb, rr, qf, d, dstride);
     else if (p.mb == kMbLarge)
       hipLaunchKernelGGL(kern4, dim3(grid), dim3(MWAVES * 64), 0, s, codes, n, (int64_t)0, q, nq, tau, cd, cc, p.capc,
@@ -2181,7 +2296,8 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
 #else
     uint16_t* mdv = nullptr;
 #endif
-    pass(hamming_mfma_swap_kernel<MFMA_MAIN>, hamming_mfma_kernel<MFMA_MAIN, kMbLarge>,
+    pass(hamming_mfma_swap_kernel<MFMA_MAIN, 2, 8>, hamming_mfma_swap_kernel<MFMA_MAIN, 4, 4>,
+         hamming_mfma_kernel<MFMA_MAIN, kMbLarge>,
          hamming_mfma_kernel<MFMA_MAIN, kMbSmall>, p.nchunks * p.nqb,
          (const int32_t*)(sampled ? tau_s : tau_p), cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, none, none,
          mdv, (int64_t)0);
@@ -2198,7 +2314,8 @@ int mfma_scan_launch(const MfmaPlan& p, const uint8_t* codes, int64_t n, const u
                 (const int32_t*)qbflag, p.nchunks, p.chunk_rows, p.chunk_rows, (int64_t)RT, (uint16_t*)nullptr,
                 (int64_t)0);
     else
-      pass(hamming_mfma_swap_kernel<MFMA_RERUN>, hamming_mfma_kernel<MFMA_RERUN, kMbLarge>,
+      pass(hamming_mfma_swap_kernel<MFMA_RERUN, 2, 8>, hamming_mfma_swap_kernel<MFMA_RERUN, 4, 4>,
+           hamming_mfma_kernel<MFMA_RERUN, kMbLarge>,
            hamming_mfma_kernel<MFMA_RERUN, kMbSmall>, p.nchunks * p.nqb,
            (const int32_t*)tau_p, cand, ccnt, p.chunk_rows, p.chunk_rows, p.nchunks, (const int32_t*)rerun,
            (const int32_t*)qbflag, (uint16_t*)nullptr, (int64_t)0);

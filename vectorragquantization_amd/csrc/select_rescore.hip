@@ -268,12 +268,31 @@ __device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, 
   if (!have_s3) {
     float qv[DPL];
     load_q(qv, a.q);
-    for (int j = w; j < K3p; j += SEL_THREADS / WAVE) {
-      const int r = ord2[j];
-      uint64_t row = sh.sel[r] & ROW_MASK;
-      if (a.remap) row = (uint64_t)a.remap[row];
-      const double c = phase3_cos(qv, a.x8 + row * DIM, a.norms[row]);
-      if (l == 0) sh.s3[r] = c;
+    // CB3 survivors per wave in flight: every row's load issued before the first score
+    constexpr int NW = SEL_THREADS / WAVE, CB3 = 8;
+    for (int j0 = w; j0 < K3p; j0 += NW * CB3) {
+      int4 raw[CB3];
+      double nrm[CB3];
+#pragma unroll
+      for (int i = 0; i < CB3; ++i) {
+        const int j = j0 + NW * i;
+        raw[i] = make_int4(0, 0, 0, 0);
+        nrm[i] = 0.0;
+        if (j < K3p) {
+          uint64_t row = sh.sel[ord2[j]] & ROW_MASK;
+          if (a.remap) row = (uint64_t)a.remap[row];
+          raw[i] = phase3_load(a.x8 + row * DIM);
+          nrm[i] = a.norms[row];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CB3; ++i) {
+        const int j = j0 + NW * i;
+        if (j < K3p) {
+          const double c = phase3_from(qv, raw[i], nrm[i]);
+          if (l == 0) sh.s3[ord2[j]] = c;
+        }
+      }
     }
   }
   __syncthreads();
@@ -324,7 +343,26 @@ __global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
   const int qi = blockIdx.x;
   const int tid = threadIdx.x, w = tid / WAVE, l = lane_id();
   const ScanKeys Lq{lists + (int64_t)qi * nlp * K, suffix ? suffix + (int64_t)qi * K : nullptr, nlp * K};
-  const int Kp = select_topk(Lq, nlp + (suffix ? 1 : 0), K, sh);
+  int Kp;
+  if (nlp == 0 && suffix) {
+    // the matrix-core scan's suffix stage left one list, already the exact top-K in FAISS (dist, row)
+    // order with KEY_NONE padding after its valid prefix: taken as is
+    const uint64_t* sq = suffix + (int64_t)qi * K;
+    if (tid == 0) sh.misc[0] = 0;
+    __syncthreads();
+    int valid = 0;
+    for (int i = tid; i < K; i += SEL_THREADS) {
+      const uint64_t key = sq[i];
+      sh.sel[i] = key;
+      sh.pay[i] = i;
+      valid += key != KEY_NONE ? 1 : 0;
+    }
+    if (valid) atomicAdd(&sh.misc[0], valid);
+    __syncthreads();
+    Kp = sh.misc[0];
+  } else {
+    Kp = select_topk(Lq, nlp + (suffix ? 1 : 0), K, sh);
+  }
   if (mode == 1) {
     for (int i = tid; i < fa.kout; i += SEL_THREADS) {
       const int64_t o = (int64_t)qi * fa.kout + i;
@@ -343,11 +381,29 @@ __global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
   const float* q = qf + (int64_t)qi * DIM;
   float qv[DPL];
   load_q(qv, q);
-  for (int j = w; j < Kp; j += SEL_THREADS / WAVE) {
-    uint64_t row = sh.sel[j] & ROW_MASK;
-    if (fa.remap) row = (uint64_t)fa.remap[row];
-    const double s = phase2_dot(qv, codes + row * (DIM / 8));
-    if (l == 0) sh.s2[j] = s;
+  {  // CB2 candidates per wave in flight: every code row's load issued before the first score
+    constexpr int NW = SEL_THREADS / WAVE, CB2 = 16;
+    for (int j0 = w; j0 < Kp; j0 += NW * CB2) {
+      uint16_t cb[CB2];
+#pragma unroll
+      for (int i = 0; i < CB2; ++i) {
+        const int j = j0 + NW * i;
+        cb[i] = 0;
+        if (j < Kp) {
+          uint64_t row = sh.sel[j] & ROW_MASK;
+          if (fa.remap) row = (uint64_t)fa.remap[row];
+          cb[i] = phase2_load(codes + row * (DIM / 8));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CB2; ++i) {
+        const int j = j0 + NW * i;
+        if (j < Kp) {
+          const double s2v = phase2_from(qv, cb[i]);
+          if (l == 0) sh.s2[j] = s2v;
+        }
+      }
+    }
   }
   if (mode == 2) {
     for (int j = w; j < Kp; j += SEL_THREADS / WAVE) {

@@ -51,7 +51,8 @@ struct MfmaPlan {
   int j;                     // sampled threshold order (tau_s = d_(j) + 1); K = tau_p only
   int capc;                  // candidate capacity per (query, chunk) list
   int rows;                  // 1: the row-split small-batch kernel K1r (nq <= 128, nqb = 1)
-  int swap;                  // 1: the large-batch pass runs K1s (row sets resident) instead of K1m (MB = 4)
+  int swap;                  // the large-batch pass runs K1s (row sets resident) instead of K1m (MB = 4):
+                             // 1 = K1s<2, 8> (two waves per SIMD), 2 = K1s<4, 4> (one wave per SIMD)
   int rows_sample;           // 1: K1r also runs the dense sample pass (MB <= 2, nq <= 64)
   int mb;                    // M-blocks (32 queries) per wave of the matrix kernel: 4 or 2 (K1r: 1, 2 (lean), 4)
   int qpb;                   // queries per workgroup (128 * mb)
