@@ -173,7 +173,8 @@ def test_k1m4_hit_staging_overflow(dev, oracle_lib):
     _assert_k1m4(N_BIG, NQ, K)
     codes_t = torch.from_numpy(codes).to(dev)
     ovf, _ = _paths(codes_t, qb, K)
-    assert ovf[planted].all() and ovf.sum() == planted.size
+    # (an unplanted query's list may also overflow by chance under its sampled tau_s: exact either way)
+    assert ovf[planted].all() and ovf.sum() <= planted.size + 8
     c, D1, I1 = _phase1(codes_t, qb, K, dev)
     assert np.array_equal(c, np.full(NQ, K))
     _check(oracle_lib, codes, qb, K, D1, I1, _sel(planted, NQ))

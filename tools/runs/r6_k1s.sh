@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-r6k1s}
 mkdir -p $OUT
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 ${T1:-600} python -u -m pytest tests/test_gpu_lists.py tests/test_gpu_mfma.py tests/test_gpu_k1m_edges.py \
+timeout -k 10 ${T1:-600} python -u -m pytest ${TESTS:-tests/test_gpu_lists.py tests/test_gpu_mfma.py tests/test_gpu_k1m_edges.py} \
   tests/test_gpu_fullsize.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1 \
   || { tail -30 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log

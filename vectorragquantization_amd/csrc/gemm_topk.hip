@@ -831,8 +831,17 @@ __device__ __forceinline__ double score_row(const float (&qv)[DPL], const RowSli
 //   binary  1 row 0.89, 2 rows 0.78, 3 rows 0.75, 8 rows 1.25
 //   cosine  1 row 1.23, 2 rows 1.13, 3 rows 1.15, 8 rows 1.79
 // (more rows per round cost VGPRs and with them resident workgroups per CU).
+// Round 6: those rounds had every load under `if (row < end)`, and a load under a divergent branch gets
+// its own vmcnt(0) at the join, so the "batched" loads were issued one at a time; the loads are now
+// unconditional (rows past the end re-read the last one).
+#ifndef VRQ_SCORE_BATCH2
+#define VRQ_SCORE_BATCH2 3
+#endif
+#ifndef VRQ_SCORE_BATCH3
+#define VRQ_SCORE_BATCH3 2
+#endif
 template <int PH>
-constexpr int kScoreBatch = PH == VRQ_GEMM_BINARY ? 3 : 2;
+constexpr int kScoreBatch = PH == VRQ_GEMM_BINARY ? VRQ_SCORE_BATCH2 : VRQ_SCORE_BATCH3;
 
 // Running exact top-k over a sequence of candidate rows row_at(j), j < count: every row is scored
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
@@ -859,10 +868,12 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
       uint32_t rr[U];
       RowSlice<PH> d[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) rr[u] = j0 + NW * u < end ? (bid ? bid[j0 + NW * u - base] : row_at(j0 + NW * u)) : 0u;
+      for (int u = 0; u < U; ++u) {
+        const int64_t jj = j0 + NW * u < end ? j0 + NW * u : end - 1;  // (j0 < end)
+        rr[u] = bid ? bid[jj - base] : row_at(jj);
+      }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (j0 + NW * u < end) d[u] = load_row<PH>(c, (int64_t)rr[u]);
+      for (int u = 0; u < U; ++u) d[u] = load_row<PH>(c, (int64_t)rr[u]);  // unconditional: one wait for all
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (j0 + NW * u >= end) break;

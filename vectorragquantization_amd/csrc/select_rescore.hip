@@ -268,30 +268,32 @@ __device__ void finish_query(int Kp, bool have_s3, const FinishArgs& a, int qi, 
   if (!have_s3) {
     float qv[DPL];
     load_q(qv, a.q);
-    // CB3 survivors per wave in flight: every row's load issued before the first score
+    // CB3 survivors per wave in flight: every row's load issued before the first score.  The loads are
+    // unconditional (indices past K3p re-read the last survivor): a load under a divergent branch gets
+    // its own vmcnt(0) at the branch join, which serialises the gathers (round 6: 59 -> ? us at config 2)
     constexpr int NW = SEL_THREADS / WAVE, CB3 = 8;
     for (int j0 = w; j0 < K3p; j0 += NW * CB3) {
+      int64_t rowv[CB3];
+#pragma unroll
+      for (int i = 0; i < CB3; ++i) {
+        const int j = j0 + NW * i;
+        rowv[i] = (int64_t)(sh.sel[ord2[j < K3p ? j : K3p - 1]] & ROW_MASK);
+      }
+      if (a.remap)
+#pragma unroll
+        for (int i = 0; i < CB3; ++i) rowv[i] = a.remap[rowv[i]];
       int4 raw[CB3];
       double nrm[CB3];
 #pragma unroll
       for (int i = 0; i < CB3; ++i) {
-        const int j = j0 + NW * i;
-        raw[i] = make_int4(0, 0, 0, 0);
-        nrm[i] = 0.0;
-        if (j < K3p) {
-          uint64_t row = sh.sel[ord2[j]] & ROW_MASK;
-          if (a.remap) row = (uint64_t)a.remap[row];
-          raw[i] = phase3_load(a.x8 + row * DIM);
-          nrm[i] = a.norms[row];
-        }
+        raw[i] = phase3_load(a.x8 + rowv[i] * DIM);
+        nrm[i] = a.norms[rowv[i]];
       }
 #pragma unroll
       for (int i = 0; i < CB3; ++i) {
         const int j = j0 + NW * i;
-        if (j < K3p) {
-          const double c = phase3_from(qv, raw[i], nrm[i]);
-          if (l == 0) sh.s3[ord2[j]] = c;
-        }
+        const double c = phase3_from(qv, raw[i], nrm[i]);
+        if (j < K3p && l == 0) sh.s3[ord2[j]] = c;
       }
     }
   }
@@ -335,7 +337,8 @@ struct ScanKeys {
 
 // mode: 0 = full 3-phase; 1 = Phase I only; 2 = shard (all Kp candidates, s2 + s3, Phase-I order)
 template <class SH>
-__global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
+// (the small instance at 4 waves per SIMD: every query of a 1024-query batch resident at once)
+__global__ __launch_bounds__(SEL_THREADS, SH::kKM <= KSMALL ? 4 : 1) void select_rescore_kernel(
     const uint64_t* __restrict__ lists, int nlp, const uint64_t* __restrict__ suffix, int K,
     const uint8_t* __restrict__ codes, const int8_t* __restrict__ x8, const double* __restrict__ norms,
     const float* __restrict__ qf, int mode, FinishArgs fa) {
@@ -382,26 +385,26 @@ __global__ __launch_bounds__(SEL_THREADS) void select_rescore_kernel(
   float qv[DPL];
   load_q(qv, q);
   {  // CB2 candidates per wave in flight: every code row's load issued before the first score
-    constexpr int NW = SEL_THREADS / WAVE, CB2 = 16;
+     // (unconditional loads, as in finish_query's Phase III)
+    constexpr int NW = SEL_THREADS / WAVE, CB2 = 8;
     for (int j0 = w; j0 < Kp; j0 += NW * CB2) {
+      int64_t rowv[CB2];
+#pragma unroll
+      for (int i = 0; i < CB2; ++i) {
+        const int j = j0 + NW * i;
+        rowv[i] = (int64_t)(sh.sel[j < Kp ? j : Kp - 1] & ROW_MASK);
+      }
+      if (fa.remap)
+#pragma unroll
+        for (int i = 0; i < CB2; ++i) rowv[i] = fa.remap[rowv[i]];
       uint16_t cb[CB2];
 #pragma unroll
-      for (int i = 0; i < CB2; ++i) {
-        const int j = j0 + NW * i;
-        cb[i] = 0;
-        if (j < Kp) {
-          uint64_t row = sh.sel[j] & ROW_MASK;
-          if (fa.remap) row = (uint64_t)fa.remap[row];
-          cb[i] = phase2_load(codes + row * (DIM / 8));
-        }
-      }
+      for (int i = 0; i < CB2; ++i) cb[i] = phase2_load(codes + rowv[i] * (DIM / 8));
 #pragma unroll
       for (int i = 0; i < CB2; ++i) {
         const int j = j0 + NW * i;
-        if (j < Kp) {
-          const double s2v = phase2_from(qv, cb[i]);
-          if (l == 0) sh.s2[j] = s2v;
-        }
+        const double s2v = phase2_from(qv, cb[i]);
+        if (j < Kp && l == 0) sh.s2[j] = s2v;
       }
     }
   }
