@@ -930,7 +930,7 @@ struct FinShared {
 // goes to the fallback.  A served or abandoned query's thr becomes +inf, so a retry pass over its
 // query block records nothing for it.
 template <int PH, bool RETRY>
-__global__ __launch_bounds__(FIN_NT) void gemm_finish_kernel(const Rows c, int64_t n,
+__global__ __launch_bounds__(FIN_NT, 4) void gemm_finish_kernel(const Rows c, int64_t n,  // (<= 128 VGPRs: 2 per CU)
                                                           int64_t row_offset, const float* __restrict__ qf, int k,
                                                           const uint32_t* __restrict__ cand,
                                                           const int32_t* __restrict__ ccnt, int nchunks, int capc,

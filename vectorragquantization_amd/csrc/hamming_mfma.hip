@@ -765,10 +765,10 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
 //     v = dist - tau(q) = 2 thr - 2 acc exactly;
 //   * the test of a block's accumulators runs in the next block's MFMA shadow (two accumulator sets);
 //     hits are staged per wave and appended to the per-(query, chunk) lists at positions taken from the
-//     workgroup's per-query LDS counters (the waves share the chunk).  The stage is flushed at the first
-//     block of each row set and whenever it holds more than STG/2 entries after a block's test, so an
-//     overflow can only come from the one block just tested: it marks that block's 32 queries'
-//     lists overflowed (exact rescan), not the workgroup's 512.
+//     workgroup's per-query LDS counters (the waves share the chunk), once per row set.  The stage holds
+//     the set's query blocks' hits in block order, so a stage overflow marks only the lists of the
+//     blocks from the first one that went past its end (exact rescan), not all 512 queries' (ADVICE
+//     round 5; a flush check after every block cost the config-2 pass 2 %).
 // Two instances:
 //   * <SRB = 2, SNW = 8>: two waves per SIMD (256 registers each; 64-row sets); at the row-set switch a
 //     wave rebuilds its A fragments and seeds from the staging buffer while the SIMD's other wave runs.
@@ -792,6 +792,7 @@ constexpr double kSwapMaxPairs = 4294967296.0;
 #ifndef VRQ_K1S_RB4
 #define VRQ_K1S_RB4 0
 #endif
+
 constexpr int SQPB = 512;  // queries per workgroup (16 blocks of 32)
 template <int SRB, int SNW>
 struct SwapShape {
@@ -907,13 +908,16 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
   const uint32_t stg0 = lds_addr(stg), sdw0 = lds_addr(sdw);
   const int64_t qstride = (int64_t)nchunks * capc;
   uint64_t* const cbase = cand + ((int64_t)qbase * nchunks + chunk) * capc;  // + ql * qstride + pos
-  int nst = 0;  // staged entries (wave-uniform)
-  // staged hits -> lists; all staged entries are of rows of one row set (first row base_row), and any
-  // entry past STG was a hit of query block qblk (the one block tested since the stage last held <= STG/2)
-  auto flush = [&](int64_t base_row, int qblk) __attribute__((always_inline)) {
-    if (nst > STG) {  // the stage overflowed: that block's 32 queries' lists -> exact rescan
-      if (l < 32) lds_add32(lc0 + (uint32_t)((qblk * 32 + l) * 4), capc + 1);
+  int nst = 0;          // staged entries (wave-uniform)
+  int ovf_qb = 1 << 20;  // the first query block whose hits went past the stage's end (wave-uniform)
+  // staged hits of one row set (first row base_row) -> lists.  The stage holds the hits of the set's
+  // query blocks 0 .. nqblk-1 in block order, so entries past STG are hits of blocks ovf_qb and later:
+  // only those blocks' lists are marked overflowed (exact rescan), not the workgroup's 512 queries'.
+  auto flush = [&](int64_t base_row) __attribute__((always_inline)) {
+    if (nst > STG) {
+      for (int i = ovf_qb * 32 + l; i < nqblk * 32; i += 64) lds_add32(lc0 + (uint32_t)(i * 4), capc + 1);
       nst = STG;
+      ovf_qb = 1 << 20;
     }
     for (int i0 = 0; i0 < nst; i0 += 64) {
       const int i = i0 + l;
@@ -950,6 +954,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
             lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << SENT_V_SHIFT) | (qrow + (g & 3) + 8 * (g >> 2)));
           }
           nst += __popcll(mask);
+          if (nst > STG && qbp < ovf_qb) ovf_qb = qbp;
         }
       }
     } else {  // at most one hit per lane: it is the lane's largest register
@@ -967,6 +972,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
         lds_write32(stg0 + (uint32_t)(pos * 4), ((v + ENT_V_BIAS) << SENT_V_SHIFT) | (qrow + (g & 3) + 8 * (g >> 2)));
       }
       nst += __popcll(lanes);
+      if (nst > STG && qbp < ovf_qb) ovf_qb = qbp;
     }
   };
 
@@ -1129,10 +1135,11 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
           }
         }
         if constexpr (s == 2) {
-          // the first block of a set: every staged hit is the previous row set's; otherwise flush when the
-          // stage is over half full (the entries are this set's)
-          if (have_prev && (qbi == 0 || nst > STG / 2) && nst) flush(stage_base, prev_qb);
-          if (qbi == 0) stage_base = set_base;
+          // the first block of a set: every staged hit is the previous row set's
+          if (qbi == 0) {
+            if (have_prev && nst) flush(stage_base);
+            stage_base = set_base;
+          }
         }
         if constexpr (s == 3) {
           const int nxt = qbi + 1 < nqblk ? qbi + 1 : 0;
@@ -1164,15 +1171,19 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
     // stale staging buffer and nothing uses the result -- so that the loop body has one path and the
     // A fragments one register assignment)
     for (int k = 0; k < nmine; ++k) {
-      for (int qp = 0; qp + 2 < nqblk; qp += 2) {
-        qblock(P0{}, F{}, qp);
-        qblock(P1{}, F{}, qp + 1);
-      }
-      qblock(P0{}, F{}, nqblk - 2);
-      if constexpr (SPREAD)
+      if constexpr (SPREAD) {
+        for (int qp = 0; qp + 2 < nqblk; qp += 2) {
+          qblock(P0{}, F{}, qp);
+          qblock(P1{}, F{}, qp + 1);
+        }
+        qblock(P0{}, F{}, nqblk - 2);
         qblock(P1{}, T{}, nqblk - 1);
-      else
-        qblock(P1{}, F{}, nqblk - 1);
+      } else {  // (one copy of the pair in the loop body: the <2, 8> instance's code size and registers)
+        for (int qp = 0; qp < nqblk; qp += 2) {
+          qblock(P0{}, F{}, qp);
+          qblock(P1{}, F{}, qp + 1);
+        }
+      }
       if (!SPREAD && k + 1 < nmine) {  // switch to the next row set: its DMA landed; start the one after
         wait_vm<0>();
         retire(P0{});
@@ -1194,7 +1205,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void hamming_mfma_swap_kernel(
         const int x4 = max(max(x[12], x[13]), x[14]);
         if (__ballot(max(max(max(x0, x1), x2), max(max(x3, x4), x[15])) > thb[1])) block_hits(acc[1][RB], RB, th, prev_qb);
       });
-      if (nst) flush(stage_base, prev_qb);
+      if (nst) flush(stage_base);
     }
   }
   wait_lgkm0();

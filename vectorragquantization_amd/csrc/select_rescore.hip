@@ -208,6 +208,27 @@ __device__ int select_topk(const KeyAt& L, int nl, int K, SH& sh) {
 // on a key is stable, so equal scores keep their previous order (:296, :321).
 template <class SH>
 __device__ void stable_desc_order(const double* sc, int m, SH& sh) {
+  if (m <= SEL_THREADS) {
+    // one element per thread: its rank = #{j : (key_j, j) < (key_i, i)} over the m keys (broadcast LDS
+    // reads), then one scatter -- 3 barriers instead of a bitonic network's log^2 rounds of them
+    const int i = threadIdx.x;
+    const uint64_t ki = i < m ? desc_key_f64(sc[i]) : KEY_NONE;
+    if (i < m) sh.skey[i] = ki;
+    __syncthreads();
+    int rank = 0;
+    if (i < m)
+      for (int j = 0; j < m; ++j) {
+        const uint64_t kj = sh.skey[j];
+        rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+      }
+    __syncthreads();
+    if (i < m) {
+      sh.skey[rank] = ki;
+      sh.sidx[rank] = i;
+    }
+    __syncthreads();
+    return;
+  }
   const int np2 = next_pow2(m > 1 ? m : 1);
   for (int i = threadIdx.x; i < np2; i += SEL_THREADS) {
     sh.skey[i] = i < m ? desc_key_f64(sc[i]) : KEY_NONE;
@@ -335,6 +356,62 @@ struct ScanKeys {
   __device__ uint64_t operator[](int i) const { return i < nlpK ? lists[i] : suffix[i - nlpK]; }
 };
 
+// Phase II (:283-293) of the Kp candidates sh.sel[0..Kp) -> sh.s2, one candidate per lane.  The score is
+// a sum of 256 nibble terms: for nibble p of the packed code (dims 4p..4p+3, MSB first) and its value v,
+// T[p][v] = sum_b (bit b of v ? q[4p+b] : -q[4p+b]) -- exact in float64, like every partial sum of the
+// reference's float32 x +-1 products -- so s2 = sum_p T[p][v_p] is the same exact value as the wave-wide
+// ddot of phase2_dot, with 256 LDS lookups per candidate instead of 1024 products spread over a wave.
+// The tables cover QT_NIB nibbles at a time (16 KiB of LDS: four workgroups of the small instance per CU).
+constexpr int QT_NIB = 128;
+template <class SH>
+__device__ void phase2_nibble_tables(const float* __restrict__ q, const uint8_t* __restrict__ codes,
+                                     const int64_t* __restrict__ remap, int Kp, SH& sh, double* qtab) {
+  constexpr int NW = SEL_THREADS / WAVE;
+  const int tid = threadIdx.x, w = tid / WAVE, l = lane_id();
+  for (int jb = 0; jb < Kp; jb += SEL_THREADS) {  // candidates jb + 4 l + w (all of them when Kp <= 256)
+    const int j = jb + NW * l + w;
+    const bool live = j < Kp;
+    int64_t row = (int64_t)(sh.sel[live ? j : 0] & ROW_MASK);
+    if (remap) row = remap[row];
+    double acc = 0.0;
+    for (int half = 0; half < 256 / QT_NIB; ++half) {
+      // this half's code bytes of the lane's row (bytes 64 half .. +63), loaded before the table build
+      uint4 cw[4];
+      const uint4* src = reinterpret_cast<const uint4*>(codes + row * (DIM / 8) + half * (QT_NIB / 2));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cw[i] = src[i];
+      __syncthreads();  // (the previous half's lookups are done)
+      for (int e = tid; e < QT_NIB * 16; e += SEL_THREADS) {
+        const int p = e >> 4, v = e & 15, d0 = 4 * (half * QT_NIB + p);
+        double t = 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const double x = (double)q[d0 + b];
+          t += ((v >> (3 - b)) & 1) ? x : -x;
+        }
+        qtab[e] = t;
+      }
+      __syncthreads();
+      if (live) {
+        const uint32_t wd[16] = {cw[0].x, cw[0].y, cw[0].z, cw[0].w, cw[1].x, cw[1].y, cw[1].z, cw[1].w,
+                                 cw[2].x, cw[2].y, cw[2].z, cw[2].w, cw[3].x, cw[3].y, cw[3].z, cw[3].w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {  // byte 4k + c (little-endian in the dword): nibbles 2(4k+c), +1
+            const uint32_t byte = (wd[k] >> (8 * c)) & 0xffu;
+            const int pb = 2 * (4 * k + c);
+            acc += qtab[pb * 16 + (byte >> 4)];
+            acc += qtab[(pb + 1) * 16 + (byte & 15)];
+          }
+        }
+      }
+    }
+    if (live) sh.s2[j] = acc;
+  }
+  __syncthreads();
+}
+
 // mode: 0 = full 3-phase; 1 = Phase I only; 2 = shard (all Kp candidates, s2 + s3, Phase-I order)
 template <class SH>
 // (the small instance at 4 waves per SIMD: every query of a 1024-query batch resident at once)
@@ -380,35 +457,16 @@ __global__ __launch_bounds__(SEL_THREADS, SH::kKM <= KSMALL ? 4 : 1) void select
     if (tid == 0 && fa.out_count) fa.out_count[qi] = Kp;
     return;
   }
+#ifdef VRQ_FIN_BISECT  // timing-only probe builds (wrong results): 1 = stop after the selection
+  if (VRQ_FIN_BISECT == 1) return;
+#endif
   // Phase II for all Kp candidates (float64, :283-293)
   const float* q = qf + (int64_t)qi * DIM;
-  float qv[DPL];
-  load_q(qv, q);
-  {  // CB2 candidates per wave in flight: every code row's load issued before the first score
-     // (unconditional loads, as in finish_query's Phase III)
-    constexpr int NW = SEL_THREADS / WAVE, CB2 = 8;
-    for (int j0 = w; j0 < Kp; j0 += NW * CB2) {
-      int64_t rowv[CB2];
-#pragma unroll
-      for (int i = 0; i < CB2; ++i) {
-        const int j = j0 + NW * i;
-        rowv[i] = (int64_t)(sh.sel[j < Kp ? j : Kp - 1] & ROW_MASK);
-      }
-      if (fa.remap)
-#pragma unroll
-        for (int i = 0; i < CB2; ++i) rowv[i] = fa.remap[rowv[i]];
-      uint16_t cb[CB2];
-#pragma unroll
-      for (int i = 0; i < CB2; ++i) cb[i] = phase2_load(codes + rowv[i] * (DIM / 8));
-#pragma unroll
-      for (int i = 0; i < CB2; ++i) {
-        const int j = j0 + NW * i;
-        const double s2v = phase2_from(qv, cb[i]);
-        if (j < Kp && l == 0) sh.s2[j] = s2v;
-      }
-    }
-  }
+  __shared__ double qtab[QT_NIB * 16];
+  phase2_nibble_tables(q, codes, fa.remap, Kp, sh, qtab);
   if (mode == 2) {
+    float qv[DPL];
+    load_q(qv, q);
     for (int j = w; j < Kp; j += SEL_THREADS / WAVE) {
       uint64_t row = sh.sel[j] & ROW_MASK;
       if (fa.remap) row = (uint64_t)fa.remap[row];
@@ -434,6 +492,9 @@ __global__ __launch_bounds__(SEL_THREADS, SH::kKM <= KSMALL ? 4 : 1) void select
     return;
   }
   __syncthreads();
+#ifdef VRQ_FIN_BISECT  // 2 = stop after Phase II
+  if (VRQ_FIN_BISECT == 2) return;
+#endif
   FinishArgs a = fa;
   a.q = q;
   finish_query(Kp, false, a, qi, sh);
