@@ -1927,6 +1927,7 @@ __global__ __launch_bounds__(256) void sample_check_kernel(const int32_t* __rest
 //   some list overflowed (or neither fits) -> exact rescan of the query's suffix rows.
 constexpr int SUF_THREADS = 256;
 constexpr int SUF_CAP = 4096;
+constexpr int SUF_COFF = 2049 + 3;  // chunk offsets of the parallel list gather live in the histogram's space
 struct SufShared {
   uint32_t hist[2049 + 3];
   uint64_t buf[SUF_CAP];
@@ -2060,7 +2061,31 @@ __global__ __launch_bounds__(SUF_THREADS) void suffix_topk_kernel(const uint8_t*
   const int64_t dfix = (int64_t)tauq - ENT_V_BIAS;
   int m = -1;
   bool real_dist = false;
-  if (!overflow && total <= SUF_CAP) {
+  if (!overflow && total <= SUF_CAP && nchunks < SUF_COFF) {
+    // every list entry gathered by its own thread (entry e of chunk c = the largest c with coff[c] <= e):
+    // independent loads, all in flight at once (a per-thread loop over its chunks' entries waited for
+    // each load before its LDS store)
+    int32_t* coff = reinterpret_cast<int32_t*>(sh.hist);
+    for (int j = 0; j < CPT; ++j) {
+      const int c = tid * CPT + j;
+      if (c < nchunks) {
+        const int v = cq[c];
+        coff[c] = off;
+        off += v < capc ? v : capc;
+      }
+    }
+    if (tid == 0) coff[nchunks] = total;
+    __syncthreads();
+    for (int e = tid; e < total; e += SUF_THREADS) {
+      int lo = 0, hi = nchunks;  // coff[lo] <= e < coff[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (coff[mid] <= e) lo = mid; else hi = mid;
+      }
+      sh.buf[e] = Cq[(int64_t)lo * capc + (e - coff[lo])];
+    }
+    m = total;
+  } else if (!overflow && total <= SUF_CAP) {
     for (int j = 0; j < CPT; ++j) {
       const int c = tid * CPT + j;
       if (c < nchunks) {
@@ -2113,10 +2138,65 @@ __global__ __launch_bounds__(SUF_THREADS) void suffix_topk_kernel(const uint8_t*
     real_dist = true;
   }
   __syncthreads();
-  const int np2 = next_pow2(m > 1 ? m : 1);
-  for (int i = m + tid; i < np2; i += SUF_THREADS) sh.buf[i] = KEY_NONE;
-  __syncthreads();
-  block_bitonic_sort_u64(sh.buf, np2);
+  if (!real_dist && m > SUF_THREADS) {
+    // only the keys with v <= T (T: the K-th smallest v-field) can be among the first K: histogram, then
+    // keep those in place, so the sort below usually runs on ~K keys instead of every candidate
+    for (int i = tid; i < 2049; i += SUF_THREADS) sh.hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += SUF_THREADS) atomicAdd(&sh.hist[(uint32_t)(sh.buf[i] >> KEY_ROW_BITS)], 1u);
+    __syncthreads();
+    {  // T = the smallest v with cum(v) >= K: BPT bins per thread, one block scan
+      constexpr int BPT = (2049 + SUF_THREADS - 1) / SUF_THREADS;
+      int loc = 0;
+      for (int b = 0; b < BPT; ++b) {
+        const int d = tid * BPT + b;
+        if (d < 2049) loc += (int)sh.hist[d];
+      }
+      int tot;
+      int cum = suf_excl_scan(loc, &tot, sh.scan);
+      for (int b = 0; b < BPT; ++b) {
+        const int d = tid * BPT + b;
+        if (d >= 2049) break;
+        const int h = (int)sh.hist[d];
+        if (cum < K && cum + h >= K) sh.misc[5] = d;
+        cum += h;
+      }
+      if (tid == 0) sh.misc[7] = 0;
+    }
+    __syncthreads();
+    const uint32_t T = (uint32_t)sh.misc[5];
+    constexpr int KPT = SUF_CAP / SUF_THREADS;  // keys per thread (m <= SUF_CAP)
+    uint64_t kk[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) kk[j] = tid + j * SUF_THREADS < m ? sh.buf[tid + j * SUF_THREADS] : KEY_NONE;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (kk[j] != KEY_NONE && (uint32_t)(kk[j] >> KEY_ROW_BITS) <= T) sh.buf[atomicAdd(&sh.misc[7], 1)] = kk[j];
+    __syncthreads();
+    m = sh.misc[7];
+  }
+  if (m <= SUF_THREADS) {
+    // one key per thread: its rank among the m distinct keys (broadcast LDS reads), one scatter
+    const uint64_t ki = tid < m ? sh.buf[tid] : KEY_NONE;
+    if (tid < 4) sh.buf[m + tid] = KEY_NONE;  // padding for the 4-key reads (m <= SUF_THREADS < SUF_CAP - 4)
+    __syncthreads();
+    int rank = 0;
+    if (tid < m) {
+      for (int j = 0; j < m; j += 4) {  // four broadcast reads in flight
+        const uint64_t a = sh.buf[j], b = sh.buf[j + 1], c = sh.buf[j + 2], d = sh.buf[j + 3];
+        rank += (a < ki ? 1 : 0) + (b < ki ? 1 : 0) + (c < ki ? 1 : 0) + (d < ki ? 1 : 0);
+      }
+    }
+    __syncthreads();
+    if (tid < m) sh.buf[rank] = ki;
+    __syncthreads();
+  } else {
+    const int np2 = next_pow2(m);
+    for (int i = m + tid; i < np2; i += SUF_THREADS) sh.buf[i] = KEY_NONE;
+    __syncthreads();
+    block_bitonic_sort_u64(sh.buf, np2);
+  }
   uint64_t* o = out + (int64_t)qi * K;
   const uint64_t ROWM = (1ull << KEY_ROW_BITS) - 1;
   for (int i = tid; i < K; i += SUF_THREADS) {
