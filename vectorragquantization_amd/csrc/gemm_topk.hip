@@ -27,13 +27,12 @@
 //     the exact fallback: one workgroup scans every row.
 //
 // Work decomposition of the two matrix passes: one workgroup per CU and 256-query block; the int8
-// pieces of its queries for all of d = 1024 sit in the accumulator file (Phase III: 8 waves of 32
-// queries, two per SIMD; Phase II: 4 waves of 64).  32-row tiles stream HBM -> LDS by LDS-DMA (pieces
+// pieces of its queries for all of d = 1024 sit in the accumulator file (8 waves of 32 queries, two per
+// SIMD; Phase II ran 4 waves of 64 until round 6).  32-row tiles stream HBM -> LDS by LDS-DMA (pieces
 // spread over the MFMA shadow).  Phase III reads the int8 rows as B directly (XOR-swizzled image,
 // conflict-free ds_read_b128); Phase II expands the packed bits into 0/1 bytes once per tile (shared by
-// the four waves) in a fixed k-permutation that the prep kernel applies to the queries as well, and
-// every B fragment feeds both of a wave's M-blocks.  The threshold test of tile t-1 runs in tile t's
-// MFMA shadow.
+// the eight waves) in a fixed k-permutation that the prep kernel applies to the queries as well.  The
+// threshold test of tile t-1 runs in tile t's MFMA shadow.
 #include <math.h>
 #include <stdlib.h>
 
@@ -49,15 +48,24 @@ namespace g5 {
 //   Phase III: 8 waves (two per SIMD) of 32 queries -- a SIMD's second wave keeps its matrix core busy
 //              while the first issues its threshold tests and LDS-DMA pieces (main pass 8.8 vs 9.5 ms
 //              for 4 waves of 64 at 10M x 1024, nq = 1024, round 3);
-//   Phase II:  4 waves of 64 queries, each B fragment feeding both M-blocks.
+//   Phase II:  the same since round 6 (round 5: 4 waves of 64 queries, each B fragment feeding both
+//              M-blocks, one wave per SIMD: the matrix cores 0.57 busy at 2.36 GHz).
 // One piece (vs q/S = a + b/256 + rho) halves the MFMA work and doubles the corpus-byte reuse per
 // query at a ~4x wider threshold margin (~2K exact rescorings per query at 10M rows): 29.3 vs 40.6 ms
 // per 10M batch, both phases (round 2).
 constexpr int GQB = 256;  // queries per workgroup
+// Phase II runs the Phase-III layout (round 6): 8 waves of 32 queries, two per SIMD, each expanding half as
+// many code dwords per tile as the round-5 4-wave layout, waves 0-3 issuing the tile's DMA.  The SIMD's
+// second wave covers the waits that idled the matrix core (main pass 7.46 -> 6.8-7.1 ms at 10M x 1024,
+// profiles/r6_c5_p2w8_ab.jsonl).  VRQ_G5_P2W8=0 (A/B builds) restores 4 waves of 64 queries.
+#ifndef VRQ_G5_P2W8
+#define VRQ_G5_P2W8 1
+#endif
 template <int PH>
 struct KShape {
   static constexpr bool P3 = PH != VRQ_GEMM_BINARY;
-  static constexpr int W = P3 ? 8 : 4, MB = P3 ? 1 : 2, QW = 32 * MB, NE = 16 * MB, RPW = 32 / W;
+  static constexpr int W = (P3 || VRQ_G5_P2W8) ? 8 : 4, MB = (P3 || VRQ_G5_P2W8) ? 1 : 2, QW = 32 * MB,
+                       NE = 16 * MB, RPW = 32 / W;
   static_assert(W * QW == GQB, "query block");
 };
 // planning target for the candidates per query (the sample size follows from it), and the
@@ -279,7 +287,9 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     d.lds = smem + slot_i * PKT;
     return d;
   };
+  constexpr bool P2W8 = !P3 && KW == 8;  // Phase II on 8 waves: the tile's 32 rows DMA'd by waves 0-3
   auto issue_piece = [&](const DmaTile& d, int i) {
+    if (P2W8 && w >= 4) return;
     // (pointer arguments through locals: a compound expression here makes the host-side compile
     // silently drop the kernel's launch stub)
     if (P3 && i == RPW) {
@@ -292,6 +302,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)ld, 16, 0, 0);
   };
   auto issue_tiny = [&](int i) {  // the single tile of a chunk shorter than 32 rows: clamp rows
+    if (P2W8 && w >= 4) return;
     if (P3 && i == RPW) {
       int64_t nr = row0 + (l >> 1);
       nr = nr < row1 ? nr : row1 - 1;
@@ -308,17 +319,23 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   };
   // Phase II expansion: lane (r, h) of wave w takes code dwords 4c..4c+3 of tile row r, c = 2w + h
   // (k-steps 4c..4c+3), and writes both lane halves' fragments of each ([k-step][lane][16 B])
+  // (8 waves: lane (r, h) of wave w takes code dwords 2c, 2c+1, c = 2w + h, i.e. half of 16-B chunk w)
   const int uc = 2 * w + h;
-  const uint32_t usrc = (uint32_t)((r * 8 + (uc ^ ((r >> 1) & 7))) * 16);
+  constexpr int UD = P2W8 ? 2 : 4;  // code dwords a lane expands per tile
+  const uint32_t usrc = (uint32_t)((r * 8 + ((P2W8 ? w : uc) ^ ((r >> 1) & 7))) * 16);
   auto unpack_frag = [&](const v4i& pv, int j, uint32_t ubw) {  // j = 2i + hh
     const int i = j >> 1, hh = j & 1;
-    const uint32_t wd = (uint32_t)(i == 0 ? pv.x : i == 1 ? pv.y : i == 2 ? pv.z : pv.w);
+    uint32_t wd;
+    if constexpr (P2W8)
+      wd = (uint32_t)(i == 0 ? (h ? pv.z : pv.x) : (h ? pv.w : pv.y));
+    else
+      wd = (uint32_t)(i == 0 ? pv.x : i == 1 ? pv.y : i == 2 ? pv.z : pv.w);
     v4i f;
     f.x = (int)((wd >> (4 * hh + 0)) & 0x01010101u);
     f.y = (int)((wd >> (4 * hh + 1)) & 0x01010101u);
     f.z = (int)((wd >> (4 * hh + 2)) & 0x01010101u);
     f.w = (int)((wd >> (4 * hh + 3)) & 0x01010101u);
-    lds_write128(ubw + (uint32_t)(((4 * uc + i) * 64 + hh * 32 + r) * 16), f);
+    lds_write128(ubw + (uint32_t)(((UD * uc + i) * 64 + hh * 32 + r) * 16), f);
   };
 
   for (int t = 0; t < AHEAD && t < ntiles; ++t) {
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
   // binary u is the integer dot), so a test is one integer max per accumulator register and the flush
   // re-derives the hit bits (acc >= 0) from the still-live accumulators
   constexpr bool SEED2 = !P3 && !DENSE;
-  v16i seed[SEED2 ? 2 : 1];  // -ceil(thr) of each accumulator register's query, clamped
+  v16i seed[SEED2 ? KMB : 1];  // -ceil(thr) of each accumulator register's query, clamped
   if constexpr (SEED2) {
 #pragma unroll
     for (int e = 0; e < KNE; ++e) {
@@ -501,7 +518,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
     lds_read128(pv, sm0 + usrc);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv)::"memory");
 #pragma unroll
-    for (int j = 0; j < 8; ++j) unpack_frag(pv, j, sm0 + (uint32_t)(NP * T2));
+    for (int j = 0; j < 2 * UD; ++j) unpack_frag(pv, j, sm0 + (uint32_t)(NP * T2));
     wait_lgkm0();
   }
 
@@ -563,9 +580,10 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
       } else {
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(ring[s & (NR - 1)]) : "n"(GKS - 1 - s) : "memory");
       }
-      if constexpr (SEED2) {  // tile starts at -ceil(thr) (Phase II: two M-blocks)
+      if constexpr (SEED2) {  // tile starts at -ceil(thr) (Phase II: two M-blocks, one on 8 waves)
         acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? seed[0] : acc[p][0]);
-        acc[p][1] = mfma_i8(A[1][s], ring[s & (NR - 1)], s == 0 ? seed[SEED2 ? 1 : 0] : acc[p][1]);
+        if constexpr (KMB == 2)
+          acc[p][1] = mfma_i8(A[KMB - 1][s], ring[s & (NR - 1)], s == 0 ? seed[KMB - 1] : acc[p][1]);
       } else {
         acc[p][0] = mfma_i8(A[0][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][0]);
         if constexpr (KMB == 2) acc[p][1] = mfma_i8(A[KMB - 1][s], ring[s & (NR - 1)], s == 0 ? zero : acc[p][1]);
@@ -586,7 +604,7 @@ __global__ __launch_bounds__(KShape<PH>::W * 64, 1) void gemm_topk_kernel(
         if constexpr (s == 2)
           if (dma) issue_piece(dt, 0);
         if constexpr (s == 1) lds_read128(pv, sm0 + (uint32_t)(sl1 * T2) + usrc);
-        if constexpr (s >= 5 && s < 13) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
+        if constexpr (s >= 5 && s < 5 + 2 * UD) unpack_frag(pv, s - 5, ubn);  // pv complete since step 3
       }
       // threshold test / dense value of tile t-1, one per k-step in [EOFF, EOFF + NE)
       constexpr int EOFF = KNE == 16 ? 4 : 0;
