@@ -49,6 +49,9 @@ constexpr int BAHEAD = 3;                   // B fragments read this many groups
 constexpr int NRING = BAHEAD < 4 ? 4 : 8;   // B fragment ring (power of two > BAHEAD)
 constexpr int STG = 512;                    // per-wave staged hit entries (u32)
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
+#ifndef VRQ_K1M_STORE_AFTER_DMA  // A/B builds: K1m issues a tile's DMA before the previous tile's list stores
+#define VRQ_K1M_STORE_AFTER_DMA 0
+#endif
 // M-blocks (32 queries each) per wave: MB = 4 for large batches (512 queries per workgroup, each
 // B fragment feeds 4 MFMAs), MB = 2 below (256 per workgroup)
 template <int MB>
@@ -408,7 +411,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   auto store_flushed = [&]() __attribute__((always_inline)) {
     if (nfl) {
       const int ql = (fe >> ENT_Q_SHIFT) & 127;
+#ifndef VRQ_K1M_PROBE_NOSTORE  // timing-only probe builds (lists left incomplete)
       if (l < nfl && fpos < capc) cbase[ql * qstride + fpos] = fkey(fe, fbase);
+#endif
       nfl = 0;
     }
   };
@@ -464,7 +469,11 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     uint32_t m16 = 0;
 #pragma unroll
     for (int g = 0; g < 16; ++g) m16 |= (a[g] > hp ? 1u : 0u) << g;
+#ifdef VRQ_K1M_PROBE_NOSLOW  // timing-only probe builds (wrong lists when a lane holds two hits)
+    if (false) {
+#else
     if (__ballot((m16 & (m16 - 1)) != 0)) {  // some lane holds two or more hits (rare)
+#endif
       block_hits(a, m, pc, hp, rel7);
     } else {
       const uint64_t lanes = __ballot(m16 != 0);
@@ -522,9 +531,19 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // ntiles >= 1 (row0 < row1 above): no zero-trip path on which the seed and B-fragment reads issued
   // above would stay in flight into the epilogue (tests/isa_check.py follows every static path)
   __builtin_assume(ntiles > 0);
+  int st_prev = 0;  // VRQ_K1M_STORE_AFTER_DMA: the previous iteration issued its list stores after its DMA
+  (void)st_prev;
   for (int t = 0; t < ntiles; ++t) {
+#if VRQ_K1M_STORE_AFTER_DMA
+    // the DMA first, then the previous tile's list stores: the end-of-tile wait lets this iteration's
+    // and the previous one's stores stay in flight (they were issued after the DMA it waits for)
+    const int st_now = nfl != 0 ? 1 : 0;  // wave-uniform
+    if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
+    store_flushed();                       // previous tile's first 64 hits
+#else
     store_flushed();                       // previous tile's first 64 hits
     if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
+#endif
     const uint32_t blt = bl0 + (uint32_t)((t % NUB) * UBT);
     const uint32_t bln = bl0 + (uint32_t)(((t + 1) % NUB) * UBT);
     const uint32_t ubw = ub0 + (uint32_t)(((t + 2) % NUB) * UBT);
@@ -674,7 +693,9 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
               const float hp = 0.5f * (float)pc;
               static_for<0, MB>([&](auto M) {
                 constexpr int mm = decltype(M)::value;
+#ifndef VRQ_K1M_PROBE_NOHITS  // timing-only probe builds: no hit extraction at all
                 if (hitm[mm]) block_hits_fast(acc[nbk ^ 1][mm], mm, pc, hp, (nbk == 0 ? 32 : 64) + ri);
+#endif
               });
             }
           }
@@ -703,13 +724,27 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     // packed tile t+3 (unpacked next iteration) landed; this wave's LDS writes done
     {
       const int last = t + NPK < ntiles ? t + NPK : ntiles - 1;  // last tile issued so far
+#ifndef VRQ_K1M_PROBE_NOVMWAIT  // timing-only probe builds (wrong results)
+#if VRQ_K1M_STORE_AFTER_DMA
+      // stores issued after the DMA of tile t+3: the previous iteration's and this one's (0..2)
+      const int nst_after = st_prev + st_now;
+      if (last - (t + 3) <= 0) wait_vm<0>();
+      else if (nst_after == 0) wait_vm<GPW>();
+      else if (nst_after == 1) wait_vm<GPW + 1>();
+      else wait_vm<GPW + 2>();
+      st_prev = st_now;
+#else
       wait_tiles(last - (t + 3));
+#endif
+#endif
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fpos), "+v"(fe)::"memory");
     fbase = row0 + (int64_t)(t - 1) * RT;
     if (nst > 64) flush_from(64, fbase);  // rare: more than 64 hits in one tile
     nst = 0;
+#ifndef VRQ_K1M_PROBE_NOBARRIER  // timing-only probe builds (wrong results)
     barrier_all();  // B_{t+1}
+#endif
   }
   store_flushed();
   if (ntiles > 0) {  // n-block 1 of the last tile
