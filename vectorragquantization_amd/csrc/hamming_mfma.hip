@@ -49,8 +49,8 @@ constexpr int BAHEAD = 3;                   // B fragments read this many groups
 constexpr int NRING = BAHEAD < 4 ? 4 : 8;   // B fragment ring (power of two > BAHEAD)
 constexpr int STG = 512;                    // per-wave staged hit entries (u32)
 constexpr int FMT_FP4 = 4;                  // e2m1 operand format of the f8f6f4 MFMA
-#ifndef VRQ_K1M_STORE_AFTER_DMA  // A/B builds: K1m issues a tile's DMA before the previous tile's list stores
-#define VRQ_K1M_STORE_AFTER_DMA 0
+#ifndef VRQ_K1M_DMA_AHEAD  // A/B builds: K1m refills a packed slot one iteration earlier (two tiles of DMA lead)
+#define VRQ_K1M_DMA_AHEAD 0
 #endif
 // M-blocks (32 queries each) per wave: MB = 4 for large batches (512 queries per workgroup, each
 // B fragment feeds 4 MFMAs), MB = 2 below (256 per workgroup)
@@ -531,15 +531,17 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
   // ntiles >= 1 (row0 < row1 above): no zero-trip path on which the seed and B-fragment reads issued
   // above would stay in flight into the epilogue (tests/isa_check.py follows every static path)
   __builtin_assume(ntiles > 0);
-  int st_prev = 0;  // VRQ_K1M_STORE_AFTER_DMA: the previous iteration issued its list stores after its DMA
+  int st_prev = 0;  // VRQ_K1M_DMA_AHEAD: the previous iteration issued list stores
   (void)st_prev;
   for (int t = 0; t < ntiles; ++t) {
-#if VRQ_K1M_STORE_AFTER_DMA
-    // the DMA first, then the previous tile's list stores: the end-of-tile wait lets this iteration's
-    // and the previous one's stores stay in flight (they were issued after the DMA it waits for)
-    const int st_now = nfl != 0 ? 1 : 0;  // wave-uniform
-    if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
+#if VRQ_K1M_DMA_AHEAD
+    // the packed slot of tile t+1 is free once tile t+1 was unpacked (iteration t-1): tile t+5 goes there
+    // now, one iteration earlier than a refill of tile t's own slot (iteration 0 also issues tile 4 into
+    // tile 0's slot, unpacked in the prologue) -- two tile-times of DMA lead for the end-of-tile wait
+    const int st_now = nfl != 0 ? 1 : 0;  // wave-uniform: this iteration issues list stores
     store_flushed();                       // previous tile's first 64 hits
+    if (t == 0 && NPK < ntiles) issue(NPK);
+    if (t + NPK + 1 < ntiles) issue(t + NPK + 1);
 #else
     store_flushed();                       // previous tile's first 64 hits
     if (t + NPK < ntiles) issue(t + NPK);  // into the slot of tile t (unpacked in iteration t-2)
@@ -723,24 +725,31 @@ __global__ __launch_bounds__(MWAVES * 64, 1) void hamming_mfma_kernel(
     pcvP = pcv[1];
     // packed tile t+3 (unpacked next iteration) landed; this wave's LDS writes done
     {
-      const int last = t + NPK < ntiles ? t + NPK : ntiles - 1;  // last tile issued so far
 #ifndef VRQ_K1M_PROBE_NOVMWAIT  // timing-only probe builds (wrong results)
-#if VRQ_K1M_STORE_AFTER_DMA
-      // stores issued after the DMA of tile t+3: the previous iteration's and this one's (0..2)
-      const int nst_after = st_prev + st_now;
-      if (last - (t + 3) <= 0) wait_vm<0>();
-      else if (nst_after == 0) wait_vm<GPW>();
-      else if (nst_after == 1) wait_vm<GPW + 1>();
-      else wait_vm<GPW + 2>();
+#if VRQ_K1M_DMA_AHEAD
+      // issued after tile t+3's DMA: the k tiles after it and the list stores of this iteration and the
+      // previous one (each store instruction sits before its iteration's DMA; rare-path stores are drained)
+      const int last = t + NPK + 1 < ntiles ? t + NPK + 1 : ntiles - 1;
+      const int k = last - (t + 3), ns = st_prev + st_now;
+      if (k <= 0) wait_vm<0>();
+      else if (k == 1) {
+        if (ns == 0) wait_vm<GPW>(); else if (ns == 1) wait_vm<GPW + 1>(); else wait_vm<GPW + 2>();
+      } else {
+        if (ns == 0) wait_vm<2 * GPW>(); else if (ns == 1) wait_vm<2 * GPW + 1>(); else wait_vm<2 * GPW + 2>();
+      }
       st_prev = st_now;
 #else
+      const int last = t + NPK < ntiles ? t + NPK : ntiles - 1;  // last tile issued so far
       wait_tiles(last - (t + 3));
 #endif
 #endif
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fpos), "+v"(fe)::"memory");
     fbase = row0 + (int64_t)(t - 1) * RT;
-    if (nst > 64) flush_from(64, fbase);  // rare: more than 64 hits in one tile
+    if (nst > 64) {  // rare: more than 64 hits in one tile
+      flush_from(64, fbase);
+      if (VRQ_K1M_DMA_AHEAD) wait_vm<0>();  // (drained: the next waits count only the per-tile stores)
+    }
     nst = 0;
 #ifndef VRQ_K1M_PROBE_NOBARRIER  // timing-only probe builds (wrong results)
     barrier_all();  // B_{t+1}
