@@ -192,18 +192,15 @@ def test_mfma_hit_staging_overflow(dev, oracle_lib, nq):
     assert np.array_equal(I0, I1)
 
 
-def _sample_rows(n, nq):
-    """Rows of the dense threshold sample, mirroring mfma_plan (hamming_mfma.hip): S = n/32 rows
-    clamped to [32768, 2^20], as 64-row tiles spread at a tile stride ts >= 64 over the corpus, in
-    256/nqb chunks of T tiles (nqb = 256-query blocks of the sample pass; for <= 64 queries the row-split
-    kernel's own sample pass: one chunk per wave, two workgroups of four waves per CU = 2048 chunks)."""
-    nqb = (nq + 255) // 256
-    S = min(max(n // 32, 32768), 1 << 20) if n // 32 <= (1 << 20) else 1 << 20
-    tiles = min(max(S // 64, 1), n // 64)
-    # batches of <= 64 queries: the row-split kernel's sample pass, one chunk per wave (2048)
-    nsc = min(2048 if nq <= 64 else max(1, 256 // nqb), tiles)
-    tiles = nsc * (tiles // nsc)
-    ts = (n - 64) // (tiles - 1) if tiles > 1 else 64
+def _sample_rows(n, nq, K=100):
+    """Rows of the dense threshold sample, from the library's own plan (vrq_scan_sample_plan): tile
+    i = c * T + t of the sample starts at row i * ts (64-row tiles spread over the corpus; for <= 64
+    queries the row-split kernel's own sample pass)."""
+    from vectorragquantization_amd import _native as N
+    info = np.zeros(8, np.int64)
+    N.check(N.load().vrq_scan_sample_plan(n, 1024, nq, K, 0, info.ctypes.data), "sample plan")
+    chunks, crows, ts = int(info[1]), int(info[2]), int(info[4])
+    tiles = chunks * (crows // 64)
     return (np.arange(tiles)[:, None] * ts + np.arange(64)[None, :]).reshape(-1)
 
 

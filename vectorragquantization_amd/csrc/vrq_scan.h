@@ -32,7 +32,13 @@ int scan_launch(const ScanPlan& p, const uint8_t* codes, int64_t n, int cb, cons
 
 // ---- K1m: matrix-core scan for large query batches (hamming_mfma.hip) ----
 constexpr int kMfmaMaxK = 128;           // K bound of the path
-constexpr int64_t kMfmaMinSample = 131072;  // (the sample pass writes lane minima only: a larger sample is cheap)
+// the minimum dense sample (VRQ_MIN_SAMPLE: A/B builds).  Round 6: 65 536 rows; with the round-6 suffix and
+// finish a looser tau_s costs less than the sample rows it saves (config 2: step 0.459-0.468 -> 0.445-0.450 ms,
+// sample pass 0.075 -> 0.048 ms, matrix pass +0.007 ms; profiles/r6_c2_min_sample_ab.jsonl)
+#ifndef VRQ_MIN_SAMPLE
+#define VRQ_MIN_SAMPLE 65536
+#endif
+constexpr int64_t kMfmaMinSample = VRQ_MIN_SAMPLE;
 constexpr int64_t kMfmaMaxSample = 1 << 20;   // dense-sample cap (1M rows: ~0.3 ms of MFMA at nq = 1024)
 constexpr int64_t kMfmaMinRows = 65536;  // below this the wavefront scan is used
 constexpr int kMfmaMinQueries = 1;       // auto-selection threshold on the batch size (K1r below 129)
