@@ -85,6 +85,44 @@ __device__ __forceinline__ double flat_ip(const float (&qv)[DPL], const float* _
   return flat_from(qv, flat_load(xrow));
 }
 
+// Phase II by nibble tables (one row per thread): tab[p * 16 + v] = sum over the 4 dims 4p .. 4p+3 of
+// nibble p (packbits MSB first) of (bit of v ? q : -q), in float64 -- exact, as every partial sum of the
+// reference's float32 x +-1 products is -- so the 256-term sum over a code's nibbles is the same exact
+// value as phase2_dot.  phase2_table fills the 32 KiB table with a block's `nthreads` threads.
+__device__ __forceinline__ void phase2_table(const float* __restrict__ q, double* tab, int tid, int nthreads) {
+  for (int e = tid; e < 256 * 16; e += nthreads) {
+    const int p = e >> 4, v = e & 15;
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const double x = (double)q[4 * p + b];
+      t += ((v >> (3 - b)) & 1) ? x : -x;
+    }
+    tab[e] = t;
+  }
+}
+__device__ __forceinline__ double phase2_nibbles(const double* tab, const uint8_t* __restrict__ code_row) {
+  const uint4* src = reinterpret_cast<const uint4*>(code_row);
+  uint4 cw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cw[i] = src[i];
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t wd[4] = {cw[i].x, cw[i].y, cw[i].z, cw[i].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // byte 16 i + 4 k + c (little-endian in the dword): nibbles 2b, 2b + 1
+        const uint32_t byte = (wd[k] >> (8 * c)) & 0xffu;
+        const int pb = 2 * (16 * i + 4 * k + c);
+        s += tab[pb * 16 + (byte >> 4)];
+        s += tab[(pb + 1) * 16 + (byte & 15)];
+      }
+  }
+  return s;
+}
+
 __device__ __forceinline__ void load_q(float (&qv)[DPL], const float* __restrict__ q) {
   const int l = lane_id();
   const float4* p = reinterpret_cast<const float4*>(q + DPL * l);

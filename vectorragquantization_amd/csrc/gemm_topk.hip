@@ -865,9 +865,12 @@ constexpr int kScoreBatch = PH == VRQ_GEMM_BINARY ? VRQ_SCORE_BATCH2 : VRQ_SCORE
 // exactly (one wave per row); a row enters the LDS sort only if it beats the current k-th by
 // (score desc, row asc), so the sort runs rarely once the list is full.  key/row[0..kc) hold the
 // running list in order.  All threads of the block call it; returns kc = min(k, count).
+// Binary (Phase II) with `qtab` (phase2_table of the query): one candidate row per THREAD, scored by the
+// nibble table (256 LDS lookups; round 6) instead of one row per wave.
 template <int PH, int NW = 4, class RowAt>
 __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL], const Rows& c, int k,
-                            uint64_t* key, uint32_t* row, int32_t* fill, uint32_t* bid = nullptr) {
+                            uint64_t* key, uint32_t* row, int32_t* fill, uint32_t* bid = nullptr,
+                            const double* qtab = nullptr) {
   constexpr int NT = NW * WAVE;
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
   if (tid == 0) *fill = 0;
@@ -882,7 +885,20 @@ __device__ int running_topk(int64_t count, RowAt row_at, const float (&qv)[DPL],
       for (int64_t j = base + tid; j < end; j += NT) bid[j - base] = row_at(j);
       __syncthreads();
     }
-    for (int64_t j0 = base + w; j0 < end; j0 += NW * U) {  // this wave: j0, j0 + NW, ... (wave-uniform)
+    if constexpr (PH == VRQ_GEMM_BINARY) {
+      if (qtab) {  // one candidate per thread
+        for (int64_t j = base + tid; j < end; j += NT) {
+          const uint32_t rr = bid ? bid[j - base] : row_at(j);
+          const uint64_t key_r = desc_key_f64(phase2_nibbles(qtab, c.codes + (int64_t)rr * (DIM / 8)));
+          if (kc < k || key_r < kk || (key_r == kk && rr < kr)) {
+            const int i = kc + atomicAdd(fill, 1);
+            key[i] = key_r;
+            row[i] = rr;
+          }
+        }
+      }
+    }
+    for (int64_t j0 = base + w; j0 < end && !(PH == VRQ_GEMM_BINARY && qtab); j0 += NW * U) {  // one row per wave
       uint32_t rr[U];
       RowSlice<PH> d[U];
 #pragma unroll
@@ -1029,7 +1045,13 @@ __global__ __launch_bounds__(FIN_NT, 4) void gemm_finish_kernel(const Rows c, in
   };
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  const int kc = running_topk<PH, FIN_NW>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2], sh.bid);
+  __shared__ double qtab[PH == VRQ_GEMM_BINARY ? 256 * 16 : 1];
+  if constexpr (PH == VRQ_GEMM_BINARY) {
+    phase2_table(qf + (int64_t)q * DIM, qtab, tid, FIN_NT);
+    __syncthreads();
+  }
+  const int kc = running_topk<PH, FIN_NW>(total, row_at, qv, c, k, sh.key, sh.row, &sh.misc[2], sh.bid,
+                                          PH == VRQ_GEMM_BINARY ? qtab : nullptr);
   if (!RETRY && sh.misc[1]) {  // overflow: raise the threshold to the recorded k-th score, retry
     if (tid == 0) {
       const double sk = desc_key_inv(sh.key[kc - 1]);
@@ -1077,8 +1099,13 @@ __global__ __launch_bounds__(256) void gemm_fallback_kernel(const Rows c, int64_
   }
   float qv[DPL];
   load_q(qv, qf + (int64_t)q * DIM);
-  const int kc =
-      running_topk<PH>(n, [](int64_t j) { return (uint32_t)j; }, qv, c, k, key, row, &fill);
+  __shared__ double qtab[PH == VRQ_GEMM_BINARY ? 256 * 16 : 1];
+  if constexpr (PH == VRQ_GEMM_BINARY) {
+    phase2_table(qf + (int64_t)q * DIM, qtab, tid, 256);
+    __syncthreads();
+  }
+  const int kc = running_topk<PH>(n, [](int64_t j) { return (uint32_t)j; }, qv, c, k, key, row, &fill, nullptr,
+                                  PH == VRQ_GEMM_BINARY ? qtab : nullptr);
   for (int i = tid; i < k; i += 256) {
     const int64_t o = (int64_t)q * k + i;
     out_rows[o] = i < kc ? (int64_t)row[i] + row_offset : -1;
