@@ -855,8 +855,8 @@ __device__ __forceinline__ double score_row(const float (&qv)[DPL], const RowSli
 #ifndef VRQ_SCORE_BATCH2
 #define VRQ_SCORE_BATCH2 3
 #endif
-#ifndef VRQ_SCORE_BATCH3
-#define VRQ_SCORE_BATCH3 2
+#ifndef VRQ_SCORE_BATCH3  // round 6, with the loads truly in flight together: 2 / 4 / 6 rows -> cosine
+#define VRQ_SCORE_BATCH3 6  // finish 0.77-0.80 / 0.74-0.75 / 0.72-0.74 ms (profiles/r6_c5_cosine_batch_ab.jsonl)
 #endif
 template <int PH>
 constexpr int kScoreBatch = PH == VRQ_GEMM_BINARY ? VRQ_SCORE_BATCH2 : VRQ_SCORE_BATCH3;
