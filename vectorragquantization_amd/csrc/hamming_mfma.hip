@@ -1796,7 +1796,11 @@ __global__ __launch_bounds__(MWAVES * 64, LeanShape<MB>::OCC) void hamming_mfma_
     static_for<0, KS>([&](auto S) {
       constexpr int s = decltype(S)::value;
       const uint32_t wd = (uint32_t)rb[s >> 2][s & 3];
+#ifdef VRQ_K1R_PROBE_NOUNPACK  // timing-only probe builds (wrong results): the packed word as the B operand
+      const v4i bfrag = {(int)wd, (int)wd, (int)wd, (int)wd};
+#else
       const v4i bfrag = unpack_row32(wd);
+#endif
       static_for<0, MB>([&](auto M) {
         constexpr int m = decltype(M)::value;
         if constexpr (s == 0 && DENSE)
