@@ -575,6 +575,28 @@ class C5Pipeline:
         return d
 
 
+def c5_candidates(P):
+    """Candidates per query each MAIN pass hands its FINISH (the count next to the
+    time): one SAMPLE + MAIN per mode after the timed region, on the pipeline's own workspace, then the
+    per-(query, chunk) list lengths (vrq_gemm_topk_layout); an overflowed list counts as its capacity."""
+    st = N.stream_handle(P.codes.device)
+    nq, m = P.qf.shape[0], P.codes.shape[0]
+    res = {}
+    for mode, name in ((N.VRQ_GEMM_BINARY, "binary"), (N.VRQ_GEMM_INT8_COSINE, "int8_cosine")):
+        plan, lay = np.zeros(8, np.int64), np.zeros(8, np.int64)
+        N.check(P.lib.vrq_gemm_topk_plan(mode, m, 1024, nq, P.k, plan.ctypes.data), "plan")
+        N.check(P.lib.vrq_gemm_topk_layout(mode, m, 1024, nq, P.k, lay.ctypes.data), "layout")
+        nch, capc, off = int(plan[1]), int(plan[2]), int(lay[2])
+        for stage in (N.VRQ_GEMM_STAGE_SAMPLE, N.VRQ_GEMM_STAGE_MAIN):
+            P._call(mode, stage, st)
+        torch.cuda.synchronize()
+        cnt = P.ws[off:off + 4 * nq * nch].view(torch.int32).view(nq, nch)
+        per_q = cnt.clamp(max=capc).sum(1).double()
+        res[name] = {"mean": float(per_q.mean()), "max": int(per_q.max()), "min": int(per_q.min()),
+                     "lists_overflowed": int((cnt > capc).sum()), "chunks": nch, "list_capacity": capc}
+    return res
+
+
 def cpu_baseline_c5(codes_h, x8_h, qf_h, k, n, nq_s=4, threads=16):
     """Reference arithmetic on the host (NumPy): Phase-II float64 GEMV over 2*unpackbits-1 and Phase-III
     float32 dot / float64 norm for every row, stable desc top-k -- on nq_s queries x the given leading
@@ -753,6 +775,7 @@ def run_c5(a, world, rank, dev):
         out["cpu_baseline"] = cpu_baseline_c5(codes[:rs].cpu().numpy(), x8[:rs].cpu().numpy(), qf.cpu().numpy(),
                                               a.k, m, threads=cpu_threads(a))
         out["cpu_gpu_identity"] = c5_identity(codes, x8, qf, P.final, a.k, cpu_threads(a))
+    out["candidates_per_query"] = c5_candidates(P)  # (after every check of P's outputs: it reuses P's workspace)
     emit(out)
     if world > 1:
         dist.barrier()
