@@ -84,7 +84,10 @@ constexpr int T2 = GRT * 128;        // Phase-II packed tile (4 KiB)
 constexpr int U2 = GKS * 1024;       // Phase-II unpacked tile [k-step][lane][16 B] (32 KiB)
 // tile schedule: B fragments read BA k-steps ahead; the LDS-DMA pieces of the tile AHEAD tiles
 // ahead issue every DS k-steps from k-step 2 (round 3 sweeps of both moved nothing)
-constexpr int BA = 2, DS = 3;
+#ifndef VRQ_G5_BA  // (round 6, 8-wave Phase II: BA = 3 costs 0.45 ms (Phase II) and 0.55 ms (Phase III) per main
+#define VRQ_G5_BA 2   // pass, profiles/r6_c5_ba3_ab.jsonl)
+#endif
+constexpr int BA = VRQ_G5_BA, DS = 3;
 
 // main-pass chunks per (CU, query block): 4 keeps the query blocks that stream the same chunk
 // within L2 reach of each other (PMC bytes 1.1x algorithmic vs 1.9x at 1, equal time; round 2)
